@@ -1,0 +1,229 @@
+"""Benchmark of the MPVAE probit-ELBO hot path on MI355X.
+
+One step = one ``compute_loss`` forward + backward (reference mpvae.py:145-210
+and its autograd) over one synthetic batch, with the probit noise generated on
+the device (philox mode), inputs resident in HBM.  Metric (BASELINE.json):
+probit MC label-samples/s = n_sample x B x L per step, whole job.
+
+Default workload (north star): C4 -- B=512, n_sample=4096 per GPU, L=z=1024.
+With --gpus N each rank evaluates its own 4096 samples of an n_sample=4096*N
+estimate (weak scaling), exchanging only the exact log-sum-exp statistics and
+gradient sums (mpvae_dist.py).
+
+    python bench.py [--gpus N --steps K --warmup W --config c4|c2|c3|c5]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import mpvae  # noqa: E402
+import mpvae_hip as H  # noqa: E402
+
+METRIC = "probit MC label-samples/sec (B×n_sample×L) at 1/2/4/8 GPU; ELBO rel-err"
+FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec
+
+# name: (L, z, B, n_sample per GPU (weak) or total (strong), d, nll_coeff, c_coeff, scaling)
+CONFIGS = {
+    "c2": (38, 38, 128, 1000, 50, 0.5, 10.0, "weak"),
+    "c3": (81, 81, 256, 2000, 50, 0.1, 200.0, "weak"),
+    "c4": (1024, 1024, 512, 4096, 50, 0.1, 200.0, "weak"),
+    "c5": (4096, 4096, 512, 8192, 50, 0.1, 200.0, "strong"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def make_inputs(L, z, B, d, device, seed=1234):
+    g = torch.Generator(device=device).manual_seed(seed)
+    y = (torch.rand((B, L), device=device, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1.0, 0.0      # no degenerate rows
+    leaves = dict(
+        fe_out=torch.randn((B, L), device=device, generator=g),
+        fe_mu=torch.randn((B, d), device=device, generator=g),
+        fe_logvar=0.1 * torch.randn((B, d), device=device, generator=g),
+        fx_out=torch.randn((B, L), device=device, generator=g),
+        fx_mu=torch.randn((B, d), device=device, generator=g),
+        fx_logvar=0.1 * torch.randn((B, d), device=device, generator=g),
+        r_sqrt_sigma=(torch.rand((L, z), device=device, generator=g, dtype=torch.float64) * 2 - 1)
+        * (6.0 / (L + z)) ** 0.5,
+    )
+    for v in leaves.values():
+        v.requires_grad_(True)
+    return y, leaves
+
+
+ORDER = ["fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar", "r_sqrt_sigma"]
+
+
+def step(y, leaves, args, it):
+    for v in leaves.values():
+        v.grad = None
+    args.mpvae_seed = 0x5EED0000 + it
+    out = mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
+    out[0].backward()
+    return out
+
+
+def roofline(times, S_local, B, L, z, steps):
+    """Dominant kernel's achieved rate vs its bound, from in-library HIP events."""
+    work = {  # algorithmic work per launch
+        "probit_fwd": ("mfma", 2.0 * S_local * B * L * z, FP32_MFMA_PEAK, "TFLOP/s"),
+        "dR_gemm": ("mfma", 2.0 * S_local * B * L * z, FP32_MFMA_PEAK, "TFLOP/s"),
+        "bwd_elem": ("hbm", 8.0 * S_local * B * L, HBM_PEAK, "GB/s"),
+        "noise_philox": ("hbm", 4.0 * S_local * B * z, HBM_PEAK, "GB/s"),
+    }
+    dom = max(times, key=lambda k: times[k][1])
+    n, ms = times[dom]
+    avg_s = ms / n / 1e3
+    if dom in work:
+        bound, per_launch, peak, unit = work[dom]
+        scale = 1e12 if unit == "TFLOP/s" else 1e9
+        achieved = per_launch / avg_s / scale
+        pk = peak / scale
+        frac = achieved / pk
+    else:
+        bound, achieved, pk, unit, frac = "unknown", None, None, None, None
+    breakdown = {k: round(v[1] / v[0], 4) for k, v in sorted(times.items(),
+                                                                 key=lambda kv: -kv[1][1])}
+    return {"kernel": dom, "bound": bound, "achieved": achieved, "peak": pk, "unit": unit,
+            "frac": frac, "traffic": None, "avg_ms": round(avg_s * 1e3, 4),
+            "per_launch_ms": breakdown}
+
+
+def cpu_baseline(L, z, B, d, S_cpu, reps, device):
+    """Reference algorithm restated in torch (oracle/torch_ref.py) on the host
+    cores, fwd+bwd on a bounded slice of the workload; also the ELBO rel-err of
+    the GPU path on the same slice."""
+    sys.path.insert(0, ROOT)
+    from oracle import torch_ref
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(99)
+    y = (torch.rand((B, L), generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1.0, 0.0
+    mk = lambda *s: torch.randn(*s, generator=g)
+    base = dict(fe_out=mk(B, L), fe_mu=mk(B, d), fe_logvar=0.1 * mk(B, d), fx_out=mk(B, L),
+                fx_mu=mk(B, d), fx_logvar=0.1 * mk(B, d),
+                r_sqrt_sigma=(torch.rand((L, z), generator=g, dtype=torch.float64) * 2 - 1)
+                * (6.0 / (L + z)) ** 0.5)
+    noise = mk(S_cpu, B, z)
+    best = float("inf")
+    cpu_out = None
+    for _ in range(reps):
+        leaves = {k: v.clone().requires_grad_(True) for k, v in base.items()}
+        t0 = time.perf_counter()
+        out = torch_ref.elbo_naive(y, *[leaves[k] for k in ORDER], noise, 0.1, 200.0)
+        out[0].backward()
+        best = min(best, time.perf_counter() - t0)
+        cpu_out = (out[0].detach(), leaves["fe_out"].grad, leaves["r_sqrt_sigma"].grad)
+    # same slice on the GPU path (explicit noise) -> ELBO rel-err
+    gl = {k: v.to(device).requires_grad_(True) for k, v in base.items()}
+    a = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_cpu, n_test_sample=S_cpu,
+                           mode="train", nll_coeff=0.1, c_coeff=200.0, mpvae_noise=noise)
+    out = mpvae.compute_loss(y.to(device), *[gl[k] for k in ORDER], a)
+    out[0].backward()
+    rel = lambda p, q: float((p.detach().cpu().double() - q.double()).abs().max()
+                             / q.double().abs().max())
+    errs = {"total": rel(out[0], cpu_out[0]), "d_fe_out": rel(gl["fe_out"].grad, cpu_out[1]),
+            "d_r_sqrt_sigma": rel(gl["r_sqrt_sigma"].grad, cpu_out[2])}
+    return {"value": S_cpu * B * L / best, "unit": "label-samples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"B={B} L=z={L} n_sample={S_cpu} fwd+bwd, oracle/torch_ref.elbo_naive "
+                      f"(reference algorithm, O(S*B*L^2) ranking tensor), best of {reps}, "
+                      f"{best:.2f} s/rep"}, errs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-s", type=int, default=2)
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    cli = ap.parse_args()
+
+    world, rank, local = setup_dist()
+    if world != cli.gpus:
+        log(f"warning: --gpus {cli.gpus} but WORLD_SIZE {world}; using {world}")
+    device = torch.device("cuda", local)
+    L, z, B, S, d, nllc, cc, scaling = CONFIGS[cli.config]
+    S_total = S * world if scaling == "weak" else S
+    S_local = S if scaling == "weak" else S // world
+    args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_total,
+                              n_test_sample=S_total, mode="train", nll_coeff=nllc, c_coeff=cc,
+                              mpvae_noise="philox", mpvae_shard=world > 1)
+    y, leaves = make_inputs(L, z, B, d, device)
+    lib = H.load_library()
+
+    for it in range(cli.warmup):
+        step(y, leaves, args, it)
+    torch.cuda.synchronize()
+    lib.mpv_timing_enable(1)
+    lib.mpv_timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(cli.steps):
+        out = step(y, leaves, args, 1000 + it)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.mpv_timing_enable(0)
+    times = H.kernel_times()
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    finite = bool(torch.isfinite(out[0]).item())
+    value = S_total * B * L * cli.steps / elapsed
+    rl = roofline(times, S_local, B, L, z, cli.steps)
+
+    cpu, errs = None, None
+    if rank == 0 and world == 1 and not cli.no_cpu_baseline:
+        S_cpu = max(1, min(cli.cpu_sample_s, S))
+        cpu, errs = cpu_baseline(L, z, B, d, S_cpu, cli.cpu_reps, device)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "label-samples/s", "n_gpus": world,
+            "steps": cli.steps, "warmup": cli.warmup, "ms_per_step": elapsed / cli.steps * 1e3,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{cli.config}: compute_loss fwd+bwd, B={B}, L={L}, z={z}, "
+                                   f"n_sample={S_total} ({S_local}/GPU), philox noise on device",
+                       "global_batch": B, "n_sample": S_total, "label_dim": L, "z_dim": z,
+                       "parallelism": f"n_sample-sharded x{world}"},
+            "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+/*
+ * mpvae_hip.h -- C ABI of the MI355X (gfx950) MPVAE probit-ELBO hot path.
+ *
+ * libmpvae_hip.so exports exactly the functions below: plain C types, raw
+ * device pointers, sizes, and a hipStream_t passed as `void*`.  Every call is
+ * stream-ordered and asynchronous (no host sync, no allocation: scratch comes
+ * from a caller-owned workspace); the return value is MPV_OK or an MPV_E*
+ * code, with a message in mpv_last_error() (thread-local).
+ *
+ * The reference (lliutianc/MPVAE-1) is pure PyTorch with no FFI; each entry
+ * point names the reference lines whose semantics it implements.  The Python
+ * host layer (mpvae-1_amd/mpvae.py) binds them with ctypes behind the
+ * reference's own `VAE` / `compute_loss` API.
+ *
+ * Layouts (row-major, fp32 unless stated):
+ *   y, fe_out, fx_out           (B, L)          labels and the two probit means
+ *   R                           (L, z)          r_sqrt_sigma (fp64 or fp32)
+ *   eps                         (S_local, B, z) probit noise of this S-shard
+ *   T                           (B, S_local, L) t = eps . R^T, kept for backward
+ *   rowstat                     (6, B, S_local) [logp_e, logp_x, P_e, N_e, P_x, N_x]
+ *   bstat                       (6, B)          [m_e, Z_e, m_x, Z_x, csum_e, csum_x]
+ *   colsum                      (2, B, L)       [sum_s E, sum_s E_x]
+ * "_e" = label branch (E, mpvae.py:177), "_x" = feature branch (E_x, :180).
+ */
+#ifndef MPVAE_HIP_H
+#define MPVAE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPV_ABI_VERSION 1
+
+enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
+enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
+
+/* Upstream-gradient slots of the 6 scalar outputs (gscal[] index) and the
+ * matching liveness bits: a slot is live when autograd delivered a gradient
+ * for it (even 0) -- that is what makes degenerate label rows NaN, exactly as
+ * the reference's 0/0 in build_multi_classification_loss (mpvae.py:118). */
+enum mpv_gslot { MPV_G_TOTAL = 0, MPV_G_NLL, MPV_G_NLL_X, MPV_G_C, MPV_G_C_X, MPV_G_KL };
+#define MPV_LIVE(slot) (1 << (slot))
+
+typedef struct mpv_shape {
+  int64_t S_local;  /* Monte-Carlo samples held by this shard                */
+  int64_t S_total;  /* samples over all shards (n_train/n_test_sample)       */
+  int64_t s_offset; /* global index of this shard's first sample             */
+  int64_t B, L, z;  /* batch, label_dim, z_dim                               */
+} mpv_shape;
+
+int mpv_abi_version(void);
+const char* mpv_last_error(void);
+
+/* Replaces mpvae.py:162 (noise = torch.normal(0,1,(S,B,z))) in perf mode:
+ * counter-based Philox4x32-10 + Box-Muller keyed on the GLOBAL element index
+ * ((s_offset+s)*B+b)*z+k, so any S-sharding draws the same noise. */
+int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                     void* stream);
+
+/* Raw Philox4x32-10 words (known-answer tests): out[4*i..4*i+3] =
+ * philox(counter = ctr0 + i (as lo,hi,0,0), key = key). */
+int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* stream);
+
+/* Element-wise dtype conversion; replaces r_sqrt_sigma.T.float() (mpvae.py:165)
+ * and the fp32 -> fp64 cast of its gradient in autograd. */
+int mpv_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
+                void* stream);
+
+/* ---------------------------------------------------------------- forward */
+typedef struct mpv_fwd_args {
+  const float* y;
+  const float* fe_out;
+  const float* fx_out;
+  const float* R32;     /* (L,z) fp32 */
+  const float* eps;     /* (S_local,B,z) */
+  float* T;             /* (B,S_local,L) or NULL when no backward will follow */
+  float* rowstat;       /* (6,B,S_local) out */
+  float* bstat;         /* (6,B) out: this shard's statistics */
+  float* colsum;        /* (2,B,L) out: this shard's sums over s */
+  void* workspace;
+  size_t workspace_bytes;
+} mpv_fwd_args;
+
+size_t mpv_fwd_workspace_bytes(const mpv_shape* shape);
+
+/* Replaces mpvae.py:165-204 for one S-shard: the noise GEMM
+ * sample_r(_x) = eps . R^T + fe_out / fx_out (computed once for both
+ * branches), the probit decode E = Phi(u)(1-1e-6)+0.5e-6, the per-(s,b) BCE
+ * log-probability (:184-185), the ranking-loss factors (:103-123, factorised
+ * as P*N), the shard-local log-sum-exp statistics (:188-189) and the sums
+ * over s behind indiv_prob / indiv_prob_label (:203-204). */
+int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* args, void* stream);
+
+/* Exact combine of per-shard bstat gathered as (nshards,6,B) -> (6,B):
+ * M = max m_r, Z = sum Z_r exp(m_r - M), ranking sums add. */
+int mpv_bstat_combine(const float* gathered, int64_t nshards, int64_t B, float* out,
+                      void* stream);
+
+typedef struct mpv_final_args {
+  const float* bstat;   /* (6,B) global */
+  const float* colsum;  /* (2,B,L) global */
+  const float* fe_mu;   /* (B,d) */
+  const float* fe_logvar;
+  const float* fx_mu;
+  const float* fx_logvar;
+  int64_t d;
+  float nll_coeff, c_coeff;
+  float* total;  /* 0-d outputs, mpvae.py:210 order */
+  float* nll;
+  float* nll_x;
+  float* c;
+  float* c_x;
+  float* kl;
+  float* indiv_prob;        /* (B,L) = mean_s E_x  (mpvae.py:203) */
+  float* indiv_prob_label;  /* (B,L) = mean_s E    (mpvae.py:204) */
+} mpv_final_args;
+
+/* Replaces mpvae.py:147-148 (KL), :188-190 (log-sum-exp nll), :122 (ranking
+ * mean), :203-210 (indiv_prob*, total).  `shape` gives B, L, S_total. */
+int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* args, void* stream);
+
+/* --------------------------------------------------------------- backward */
+typedef struct mpv_bwd_args {
+  const float* y;
+  const float* fe_out;
+  const float* fx_out;
+  const float* eps;            /* (S_local,B,z), the forward's noise */
+  float* T;                    /* in: forward's T; clobbered with d(sample_r)+d(sample_r_x) */
+  const float* rowstat;        /* (6,B,S_local) from the forward */
+  const float* bstat;          /* (6,B) GLOBAL statistics */
+  const float* gscal;          /* (6) device: upstream grads, mpv_gslot order */
+  const float* g_indiv;        /* (B,L) grad of indiv_prob, or NULL */
+  const float* g_indiv_label;  /* (B,L) grad of indiv_prob_label, or NULL */
+  float nll_coeff, c_coeff;
+  int live;                    /* MPV_LIVE bits of gscal */
+  float* dfe_dfx;              /* (2,B,L) out: d fe_out, d fx_out (this shard) */
+  float* dR32;                 /* (L,z) out fp32 d r_sqrt_sigma (this shard), or NULL */
+  void* workspace;
+  size_t workspace_bytes;
+} mpv_bwd_args;
+
+size_t mpv_bwd_workspace_bytes(const mpv_shape* shape);
+
+/* Replaces PyTorch autograd through mpvae.py:165-210 (including the pairwise
+ * (S,B,L,L) ranking tensor): d fe_out, d fx_out and d r_sqrt_sigma. */
+int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* args, void* stream);
+
+typedef struct mpv_kl_bwd_args {
+  const float* fe_mu;
+  const float* fe_logvar;
+  const float* fx_mu;
+  const float* fx_logvar;
+  int64_t B, d;
+  const float* gscal;  /* (6) device, mpv_gslot order; uses TOTAL and KL */
+  float* g_fe_mu;
+  float* g_fe_logvar;
+  float* g_fx_mu;
+  float* g_fx_logvar;
+} mpv_kl_bwd_args;
+
+/* Replaces autograd through the KL term, mpvae.py:147-148. */
+int mpv_kl_bwd(const mpv_kl_bwd_args* args, void* stream);
+
+/* ------------------------------------------------- reparameterisation a3 */
+typedef struct mpv_reparam_args {
+  const float* mu_e;
+  const float* logvar_e;
+  const float* eps_e;
+  float* z_e;
+  int64_t n_e;  /* elements of the label encoder (0 = skip) */
+  const float* mu_x;
+  const float* logvar_x;
+  const float* eps_x;
+  float* z_x;
+  int64_t n_x;  /* elements of the feature encoder (0 = skip) */
+} mpv_reparam_args;
+
+/* Replaces label_reparameterize / feat_reparameterize (mpvae.py:66-74):
+ * z = mu + eps * exp(0.5 logvar) for BOTH encoders in one launch. */
+int mpv_reparam_fwd(const mpv_reparam_args* args, void* stream);
+
+typedef struct mpv_reparam_bwd_args {
+  const float* gz_e;  /* NULL = no gradient reached z_e */
+  const float* logvar_e;
+  const float* eps_e;
+  float* gmu_e;
+  float* glogvar_e;
+  int64_t n_e;
+  const float* gz_x;
+  const float* logvar_x;
+  const float* eps_x;
+  float* gmu_x;
+  float* glogvar_x;
+  int64_t n_x;
+} mpv_reparam_bwd_args;
+
+int mpv_reparam_bwd(const mpv_reparam_bwd_args* args, void* stream);
+
+/* ------------------------------------------------------------ measurement */
+/* When enabled, every kernel launch of the library is bracketed by a pair of
+ * HIP events on the launch stream (bench.py's per-kernel roofline timing).
+ * Kernel names: noise_philox, probit_fwd, fwd_combine, finalize, bwd_coef,
+ * bwd_elem, dR_gemm, sum_slabs, convert, bstat_combine, reparam_fwd,
+ * reparam_bwd, kl_bwd.  Query synchronises the recorded events. */
+int mpv_timing_enable(int on);
+int mpv_timing_reset(void);
+int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPVAE_HIP_H */

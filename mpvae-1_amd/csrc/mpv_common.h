@@ -1,0 +1,100 @@
+// Shared device helpers for the MPVAE probit-ELBO kernels (gfx950 / CDNA4).
+//
+// Wave size is 64 everywhere.  Reductions inside a 16-lane MFMA row use DPP
+// row shifts (no LDS round trip); cross-row / cross-wave reductions go
+// through __shfl_xor (ds_bpermute) or LDS.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MPV_DEV __device__ __forceinline__
+
+namespace mpv {
+
+// ---- constants of the reference ELBO (mpvae.py:156,177,180,118,148) -------
+// eps1 = tensor([1e-6]).float(); E = cdf*(1-eps1) + eps1*0.5 evaluated in fp32
+constexpr float kEps1 = 1e-6f;
+constexpr float kC1 = 1.0f - kEps1;        // (1 - eps1) rounded to fp32
+constexpr float kC0 = kEps1 * 0.5f;        // eps1 * 0.5
+constexpr float kInvSqrt2 = 0.70710678118654752440f;
+constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
+constexpr float kKlEps = 1e-6f;
+constexpr float kKlWeight = 1.1f;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Probit probability of reference mpvae.py:171-180 (torch Normal.cdf).
+MPV_DEV float probit_prob(float u) {
+  float cdf = 0.5f * (1.0f + erff(u * kInvSqrt2));
+  return cdf * kC1 + kC0;
+}
+
+// ---- DPP row (16-lane) reductions ------------------------------------------
+// row_shr:n = 0x110 + n.  After the 4 steps lane 15 of every 16-lane row holds
+// the row's sum (bound_ctrl: lanes shifted in from outside the row read 0).
+template <int CTRL>
+MPV_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+MPV_DEV float row16_sum_to_lane15(float v) {
+  v += dpp_f<0x111>(v);   // row_shr:1
+  v += dpp_f<0x112>(v);   // row_shr:2
+  v += dpp_f<0x114>(v);   // row_shr:4
+  v += dpp_f<0x118>(v);   // row_shr:8
+  return v;
+}
+
+MPV_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MPV_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block reduction over up to 1024 threads; `red` must hold >= 16 floats.
+// Every thread returns the total.
+template <bool IS_MAX>
+MPV_DEV float block_reduce(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = IS_MAX ? wave_max(v) : wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = IS_MAX ? -INFINITY : 0.0f;
+  for (int i = 0; i < nw; ++i) r = IS_MAX ? fmaxf(r, red[i]) : r + red[i];
+  return r;
+}
+
+// ---- Philox4x32-10 (Salmon et al. SC'11) ------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+MPV_DEV u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Box-Muller on one word pair (see oracle/philox.py for the exact map).
+MPV_DEV void box_muller(uint32_t we, uint32_t wo, float& n0, float& n1) {
+  const float u = ((float)(we >> 8) + 0.5f) * 5.9604644775390625e-8f;   // 2^-24
+  const float v = (float)(wo >> 8) * 5.9604644775390625e-8f;
+  const float r = sqrtf(-2.0f * logf(u));
+  float s, c;
+  sincospif(2.0f * v, &s, &c);
+  n0 = r * c;
+  n1 = r * s;
+}
+
+}  // namespace mpv

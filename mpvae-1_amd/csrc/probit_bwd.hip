@@ -1,0 +1,445 @@
+// Backward of the MPVAE probit ELBO for one S-shard: the gradients PyTorch
+// autograd takes through reference mpvae.py:165-210, written out analytically.
+//
+//   bwd_coef_kernel  per (s,b): alpha = -g_nll * softmax_s(logp)/B and the
+//                    ranking coefficients betaP = g_c N/(n S B), betaN = g_c P/(n S B)
+//                    (NaN for a degenerate row whose ranking term is live,
+//                    reproducing the 0/0 of mpvae.py:118 under autograd)
+//   bwd_elem_kernel  streams T once: recomputes E, E_x, forms
+//                    dE = alpha (y/E - (1-y)/(1-E)) - [y=1] betaP e^{-5E}
+//                         + [y=0] betaN e^{5E} + g_indiv/S,
+//                    du = dE (1-1e-6) phi(u); column sums over s give d fe_out /
+//                    d fx_out; writes G = du + du_x over T.
+//   dR_gemm_kernel   dR[l][k] = sum_{s,b} G[s,b,l] eps[s,b,k] on the fp32
+//                    matrix cores, split-K over the S*B rows into slabs,
+//                    reduced in a fixed order (deterministic).
+#include "abi_util.h"
+#include "mpv_common.h"
+
+namespace mpv {
+
+int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
+                     hipStream_t s);
+
+// --------------------------------------------------------------- coefficients
+__global__ __launch_bounds__(256) void bwd_coef_kernel(const float* __restrict__ y,
+                                                      const float* __restrict__ rowstat,
+                                                      const float* __restrict__ bstat,
+                                                      const float* __restrict__ gscal,
+                                                      float* __restrict__ coef, int S, int B,
+                                                      int L, float S_total, float nll_coeff,
+                                                      float c_coeff, int live) {
+  __shared__ float red[16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float np = 0.f, nn = 0.f;
+  for (int l = tid; l < L; l += blockDim.x) {
+    const float v = y[(int64_t)b * L + l];
+    np += (v == 1.0f) ? 1.0f : 0.0f;
+    nn += (v == 0.0f) ? 1.0f : 0.0f;
+  }
+  np = block_reduce<false>(np, red);
+  nn = block_reduce<false>(nn, red);
+  const float nrm = np * nn;
+  const float gt = gscal[MPV_G_TOTAL];
+  const float gn[2] = {gscal[MPV_G_NLL] + nll_coeff * gt, gscal[MPV_G_NLL_X] + nll_coeff * gt};
+  const float gc[2] = {gscal[MPV_G_C] + c_coeff * gt, gscal[MPV_G_C_X] + c_coeff * gt};
+  const bool clive[2] = {(live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C))) != 0,
+                         (live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C_X))) != 0};
+  const float inv_B = 1.0f / (float)B;
+#pragma unroll
+  for (int br = 0; br < 2; ++br) {
+    const float M = bstat[(2 * br) * B + b], Z = bstat[(2 * br + 1) * B + b];
+    const bool dead = !(nrm > 0.0f) && clive[br];
+    const float cs = gc[br] / (nrm * S_total * (float)B);
+    for (int s = tid; s < S; s += blockDim.x) {
+      const float lp = rowstat[((int64_t)br * B + b) * S + s];
+      const float P = rowstat[((int64_t)(2 + 2 * br) * B + b) * S + s];
+      const float N = rowstat[((int64_t)(3 + 2 * br) * B + b) * S + s];
+      float alpha = -gn[br] * (expf(lp - M) / Z) * inv_B;
+      float bP = nrm > 0.0f ? cs * N : 0.0f;
+      float bN = nrm > 0.0f ? cs * P : 0.0f;
+      if (dead) alpha = bP = bN = __builtin_nanf("");
+      coef[((int64_t)(3 * br + 0) * B + b) * S + s] = alpha;
+      coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP;
+      coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN;
+    }
+  }
+}
+
+// ------------------------------------------------------------ element pass
+struct ElemParams {
+  const float* y;
+  const float* fe;
+  const float* fx;
+  const float* gI;   // (B,L) grad of indiv_prob (feature branch) or NULL
+  const float* gIL;  // (B,L) grad of indiv_prob_label (label branch) or NULL
+  const float* coef;
+  float* T;
+  float* colpart;  // [nSc][2][B][L]
+  int S, B, L;
+  int TPR, RPI, rows_per_chunk;
+  float inv_S;
+};
+
+MPV_DEV float d_elem(float t, float base, float y, bool soft, float alpha, float bP, float bN,
+                     float gind) {
+  const float u = t + base;
+  const float E = probit_prob(u);
+  // d logp / dE = y/E - (1-y)/(1-E)  (mpvae.py:184-185)
+  float dl = (y == 0.0f) ? -1.0f / (1.0f - E) : 1.0f / E;
+  if (soft) dl = y / E - (1.0f - y) / (1.0f - E);
+  float dE = alpha * dl + gind;
+  if (y == 1.0f) dE -= bP * expf(-5.0f * E);
+  if (y == 0.0f) dE += bN * expf(5.0f * E);
+  // a degenerate row poisons every label, whatever its value (reference autograd)
+  if (bP != bP) dE = bP;
+  return dE * kC1 * kInvSqrt2Pi * expf(-0.5f * u * u);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
+  __shared__ float cred[256 * 8];
+  const int b = blockIdx.x, sc = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int rsub = tid / p.TPR, cq = tid % p.TPR;
+  const bool active = rsub < p.RPI;
+  const int c0 = blockIdx.z * 1024 + cq * 4;
+  const int S = p.S, B = p.B, L = p.L;
+
+  float yv[4], fe[4], fx[4], gi[4], gil[4];
+  bool ok[4], soft[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    ok[q] = active && c < L;
+    const int64_t o = (int64_t)b * L + (ok[q] ? c : 0);
+    yv[q] = ok[q] ? p.y[o] : 0.0f;
+    fe[q] = ok[q] ? p.fe[o] : 0.0f;
+    fx[q] = ok[q] ? p.fx[o] : 0.0f;
+    gi[q] = (ok[q] && p.gI) ? p.gI[o] * p.inv_S : 0.0f;
+    gil[q] = (ok[q] && p.gIL) ? p.gIL[o] * p.inv_S : 0.0f;
+    soft[q] = !(yv[q] == 0.0f || yv[q] == 1.0f);
+  }
+  float se[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  const int s_begin = sc * p.rows_per_chunk;
+  const int s_end = min(S, s_begin + p.rows_per_chunk);
+  if (active && c0 < L) {
+    for (int s = s_begin + rsub; s < s_end; s += p.RPI) {
+      const int64_t cb = (int64_t)b * S + s;
+      const int64_t BS = (int64_t)B * S;
+      const float ae = p.coef[0 * BS + cb], pe = p.coef[1 * BS + cb], ne = p.coef[2 * BS + cb];
+      const float ax = p.coef[3 * BS + cb], px = p.coef[4 * BS + cb], nx = p.coef[5 * BS + cb];
+      float* row = p.T + cb * L;
+      float t[4];
+      if (VEC && c0 + 3 < L) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
+        t[0] = v[0]; t[1] = v[1]; t[2] = v[2]; t[3] = v[3];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = ok[q] ? row[c0 + q] : 0.0f;
+      }
+      float G[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float ge = d_elem(t[q], fe[q], yv[q], soft[q], ae, pe, ne, gil[q]);
+        const float gx = d_elem(t[q], fx[q], yv[q], soft[q], ax, px, nx, gi[q]);
+        se[q] += ge;
+        sx[q] += gx;
+        G[q] = ge + gx;
+      }
+      if (VEC && c0 + 3 < L) {
+        *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (ok[q]) row[c0 + q] = G[q];
+      }
+    }
+  }
+  // column sums over this block's rows: reduce the RPI row-lanes per column
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    cred[tid * 8 + q] = se[q];
+    cred[tid * 8 + 4 + q] = sx[q];
+  }
+  __syncthreads();
+  for (int j = tid; j < p.TPR * 4; j += blockDim.x) {
+    const int cqq = j >> 2, q = j & 3;
+    const int c = blockIdx.z * 1024 + j;
+    if (c < L) {
+      float e = 0.f, x = 0.f;
+      for (int r = 0; r < p.RPI; ++r) {
+        e += cred[(r * p.TPR + cqq) * 8 + q];
+        x += cred[(r * p.TPR + cqq) * 8 + 4 + q];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * B + b) * L + c] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * B + b) * L + c] = x;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- dR GEMM
+struct DrParams {
+  const float* G;    // (B*S, L): row q = b*S + s  (the T buffer)
+  const float* eps;  // (S, B, z)
+  float* slab;       // [nKc][L][z]
+  int S, B, L, z;
+  int nLt, nZt, nKc, rows_per_chunk;
+};
+
+constexpr int kDrBK = 32;
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
+  constexpr int WM = 2, WN = 2;
+  constexpr int BM = WM * TM * 16;  // l tile
+  constexpr int BN = WN * TN * 16;  // z tile
+  constexpr int LDG = BM + 16, LDE = BN + 16;  // conflict-free ds_read_b32 (stride = 16 mod 32)
+  constexpr int G4 = kDrBK * BM / 4, E4 = kDrBK * BN / 4;
+  constexpr int GV = (G4 + 255) / 256, EV = (E4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float smem[kDrBK * (LDG + LDE)];
+  float* Gs = smem;
+  float* Es = smem + kDrBK * LDG;
+
+  // block -> (kc, tile); all tiles of one kc share eps/G rows: same id mod 8
+  const int nT = p.nLt * p.nZt;
+  int kc, tile;
+  {
+    const int id = blockIdx.x, K = p.nKc;
+    const int full = (K / 8) * 8 * nT;
+    if (id < full) {
+      const int q = id / (8 * nT), r = id % (8 * nT);
+      tile = r / 8;
+      kc = q * 8 + (r % 8);
+    } else {
+      const int r = id - full, Kr = K % 8;
+      tile = r / Kr;
+      kc = (K / 8) * 8 + (r % Kr);
+    }
+  }
+  const int l0 = (tile / p.nZt) * BM, z0 = (tile % p.nZt) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, B = p.B, L = p.L, z = p.z;
+  const int rows = B * S;
+  const int q_begin = kc * p.rows_per_chunk;
+  const int q_end = min(rows, q_begin + p.rows_per_chunk);
+  const bool gvec = (L & 3) == 0, evec = (z & 3) == 0;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 rg[GV], re[EV];
+  auto load = [&](int q0) {
+#pragma unroll
+    for (int v = 0; v < GV; ++v) {
+      const int idx = tid + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (idx < G4) {
+        const int r = idx / (BM / 4), c = l0 + (idx % (BM / 4)) * 4;
+        const int q = q0 + r;
+        if (q < q_end) {
+          const float* src = p.G + (int64_t)q * L;
+          if (gvec && c + 3 < L) x = *reinterpret_cast<const f32x4*>(src + c);
+          else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = (c + k < L) ? src[c + k] : 0.0f;
+          }
+        }
+      }
+      rg[v] = x;
+    }
+#pragma unroll
+    for (int v = 0; v < EV; ++v) {
+      const int idx = tid + v * 256;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (idx < E4) {
+        const int r = idx / (BN / 4), c = z0 + (idx % (BN / 4)) * 4;
+        const int q = q0 + r;
+        if (q < q_end) {
+          const int bb = q / S, s = q - bb * S;
+          const float* src = p.eps + ((int64_t)s * B + bb) * z;
+          if (evec && c + 3 < z) x = *reinterpret_cast<const f32x4*>(src + c);
+          else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = (c + k < z) ? src[c + k] : 0.0f;
+          }
+        }
+      }
+      re[v] = x;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int v = 0; v < GV; ++v) {
+      const int idx = tid + v * 256;
+      if (idx < G4)
+        *reinterpret_cast<f32x4*>(&Gs[(idx / (BM / 4)) * LDG + (idx % (BM / 4)) * 4]) = rg[v];
+    }
+#pragma unroll
+    for (int v = 0; v < EV; ++v) {
+      const int idx = tid + v * 256;
+      if (idx < E4)
+        *reinterpret_cast<f32x4*>(&Es[(idx / (BN / 4)) * LDE + (idx % (BN / 4)) * 4]) = re[v];
+    }
+  };
+
+  if (q_begin < q_end) {
+    load(q_begin);
+    store();
+    __syncthreads();
+    for (int q0 = q_begin; q0 < q_end; q0 += kDrBK) {
+      const bool more = q0 + kDrBK < q_end;
+      if (more) load(q0 + kDrBK);
+#pragma unroll
+      for (int j = 0; j < kDrBK / 4; ++j) {
+        float a[TM], bb[TN];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) a[m] = Gs[(j * 4 + lg) * LDG + wm * TM * 16 + m * 16 + lr];
+#pragma unroll
+        for (int n = 0; n < TN; ++n) bb[n] = Es[(j * 4 + lg) * LDE + wn * TN * 16 + n * 16 + lr];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], bb[n], acc[m][n], 0, 0, 0);
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+  // D[i = l][j = z]: row = lg*4 + reg, col = lr
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = l0 + wm * TM * 16 + m * 16 + lg * 4 + i;
+        const int zc = z0 + wn * TN * 16 + n * 16 + lr;
+        if (l < L && zc < z) p.slab[((int64_t)kc * L + l) * z + zc] = acc[m][n][i];
+      }
+}
+
+// ------------------------------------------------------------------- plans
+struct BwdPlan {
+  int TPR, RPI, nLc, nSc, rows_per_chunk;
+  int nLt, nZt, nKc, dr_rows_per_chunk;
+  size_t coef_bytes, colpart_bytes, slab_bytes;
+};
+
+static BwdPlan plan_bwd(const mpv_shape* s) {
+  BwdPlan pl;
+  const int64_t L = s->L, S = s->S_local, B = s->B, z = s->z;
+  pl.nLc = (int)cdiv(L, 1024);
+  pl.TPR = (int)(L >= 1024 ? 256 : cdiv(L, 4));
+  pl.RPI = 256 / pl.TPR;
+  int64_t want = cdiv(2048, B * pl.nLc);
+  if (want < 1) want = 1;
+  const int64_t max_chunks = cdiv(S, pl.RPI);
+  if (want > max_chunks) want = max_chunks;
+  pl.rows_per_chunk = (int)cdiv(S, want);
+  pl.nSc = (int)cdiv(S, pl.rows_per_chunk);
+  pl.nLt = (int)cdiv(L, 128);
+  pl.nZt = (int)cdiv(z, 128);
+  const int64_t rows = B * S;
+  const int64_t tiles = (int64_t)pl.nLt * pl.nZt;
+  int64_t kc = cdiv(1536, tiles);
+  const int64_t kc_max = cdiv(rows, 256);
+  if (kc > kc_max) kc = kc_max;
+  if (kc < 1) kc = 1;
+  pl.dr_rows_per_chunk = (int)(cdiv(cdiv(rows, kc), kDrBK) * kDrBK);
+  pl.nKc = (int)cdiv(rows, pl.dr_rows_per_chunk);
+  pl.coef_bytes = align_up(sizeof(float) * 6 * (size_t)B * S, 256);
+  pl.colpart_bytes = align_up(sizeof(float) * (size_t)pl.nSc * 2 * B * L, 256);
+  pl.slab_bytes = align_up(sizeof(float) * (size_t)pl.nKc * L * z, 256);
+  return pl;
+}
+
+}  // namespace mpv
+
+using namespace mpv;
+
+extern "C" {
+
+size_t mpv_bwd_workspace_bytes(const mpv_shape* shape) {
+  if (check_shape(shape) != MPV_OK) return 0;
+  const BwdPlan pl = plan_bwd(shape);
+  return pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes;
+}
+
+int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) {
+  if (int rc = check_shape(shape)) return rc;
+  MPV_REQUIRE(a && a->y && a->fe_out && a->fx_out && a->eps && a->T && a->rowstat && a->bstat &&
+                  a->gscal && a->dfe_dfx && a->workspace,
+              "NULL pointer in mpv_bwd_args");
+  const BwdPlan pl = plan_bwd(shape);
+  const size_t need = pl.coef_bytes + pl.colpart_bytes + (a->dR32 ? pl.slab_bytes : 0);
+  MPV_REQUIRE(a->workspace_bytes >= need, "workspace too small: %zu < %zu", a->workspace_bytes,
+              need);
+  hipStream_t st = as_stream(stream);
+  char* ws = reinterpret_cast<char*>(a->workspace);
+  float* coef = reinterpret_cast<float*>(ws);
+  float* colpart = reinterpret_cast<float*>(ws + pl.coef_bytes);
+  float* slab = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes);
+  const int S = (int)shape->S_local, B = (int)shape->B, L = (int)shape->L, z = (int)shape->z;
+
+  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B), dim3(256), 0, st, a->y, a->rowstat, a->bstat,
+                     a->gscal, coef, S, B, L, (float)shape->S_total, a->nll_coeff, a->c_coeff,
+                     a->live);
+  if (int rc = check_launch("bwd_coef")) return rc;
+
+  ElemParams ep;
+  ep.y = a->y;
+  ep.fe = a->fe_out;
+  ep.fx = a->fx_out;
+  ep.gI = a->g_indiv;
+  ep.gIL = a->g_indiv_label;
+  ep.coef = coef;
+  ep.T = a->T;
+  ep.colpart = colpart;
+  ep.S = S;
+  ep.B = B;
+  ep.L = L;
+  ep.TPR = pl.TPR;
+  ep.RPI = pl.RPI;
+  ep.rows_per_chunk = pl.rows_per_chunk;
+  ep.inv_S = 1.0f / (float)shape->S_total;
+  const dim3 eg(B, pl.nSc, pl.nLc);
+  if ((L & 3) == 0)
+    MPV_LAUNCH("bwd_elem", bwd_elem_kernel<true>, eg, dim3(256), 0, st, ep);
+  else
+    MPV_LAUNCH("bwd_elem", bwd_elem_kernel<false>, eg, dim3(256), 0, st, ep);
+  if (int rc = check_launch("bwd_elem")) return rc;
+  if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
+    return rc;
+
+  if (a->dR32) {
+    DrParams dp;
+    dp.G = a->T;
+    dp.eps = a->eps;
+    dp.slab = slab;
+    dp.S = S;
+    dp.B = B;
+    dp.L = L;
+    dp.z = z;
+    dp.nLt = pl.nLt;
+    dp.nZt = pl.nZt;
+    dp.nKc = pl.nKc;
+    dp.rows_per_chunk = pl.dr_rows_per_chunk;
+    const int64_t blocks = (int64_t)pl.nLt * pl.nZt * pl.nKc;
+    MPV_LAUNCH("dR_gemm", (dR_gemm_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+    if (int rc = check_launch("dR_gemm")) return rc;
+    if (int rc = launch_sum_slabs(slab, pl.nKc, (int64_t)L * z, a->dR32, MPV_F32, st)) return rc;
+  }
+  return MPV_OK;
+}
+
+}  // extern "C"

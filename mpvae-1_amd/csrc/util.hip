@@ -1,0 +1,365 @@
+// Small kernels of the hot path: Philox noise (a7), dtype conversion (a8
+// prep / fp64 gradient), slab reductions, the cross-shard statistic combine,
+// the fused two-encoder reparameterisation (a3) and the KL backward (a5).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "abi_util.h"
+#include "mpv_common.h"
+
+namespace mpv {
+
+static thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPV_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+  return MPV_OK;
+}
+
+// ---------------------------------------------------------- launch timing
+struct TimerSlot {
+  std::string name;
+  std::vector<hipEvent_t> start, stop;
+  size_t used = 0;
+};
+static std::mutex g_tmu;
+static bool g_timing = false;
+static std::vector<TimerSlot> g_slots;
+
+TimedLaunch::TimedLaunch(const char* kernel, hipStream_t s) : s_(s) {
+  if (!g_timing) return;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  int k = -1;
+  for (size_t i = 0; i < g_slots.size(); ++i)
+    if (g_slots[i].name == kernel) k = (int)i;
+  if (k < 0) {
+    g_slots.push_back(TimerSlot{kernel, {}, {}, 0});
+    k = (int)g_slots.size() - 1;
+  }
+  TimerSlot& t = g_slots[k];
+  if (t.used == t.start.size()) {
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return;
+    if (hipEventCreate(&b) != hipSuccess) return;
+    t.start.push_back(a);
+    t.stop.push_back(b);
+  }
+  pair_ = t.used++;
+  slot_ = k;
+  (void)hipEventRecord(t.start[pair_], s_);
+}
+
+TimedLaunch::~TimedLaunch() {
+  if (slot_ < 0) return;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  (void)hipEventRecord(g_slots[slot_].stop[pair_], s_);
+}
+
+int check_shape(const mpv_shape* s) {
+  MPV_REQUIRE(s != nullptr, "shape is NULL");
+  MPV_REQUIRE(s->B > 0 && s->L > 0 && s->z > 0, "B, L, z must be positive (got %lld, %lld, %lld)",
+              (long long)s->B, (long long)s->L, (long long)s->z);
+  MPV_REQUIRE(s->S_local > 0 && s->S_total >= s->S_local && s->s_offset >= 0 &&
+                  s->s_offset + s->S_local <= s->S_total,
+              "bad sample range: S_local=%lld S_total=%lld s_offset=%lld",
+              (long long)s->S_local, (long long)s->S_total, (long long)s->s_offset);
+  MPV_REQUIRE(s->B * s->S_local < (int64_t(1) << 31), "B*S_local must fit in int32");
+  MPV_REQUIRE(s->L < (1 << 24) && s->z < (1 << 24), "L and z must be < 2^24");
+  return MPV_OK;
+}
+
+// ------------------------------------------------------------- Philox noise
+// One thread = one Philox counter = 4 consecutive noise elements.
+__global__ void noise_philox_kernel(float* __restrict__ eps, int64_t e_begin, int64_t e_count,
+                                    uint32_t k0, uint32_t k1, uint64_t offset) {
+  const int64_t g0 = e_begin >> 2;  // first counter touching the shard
+  const int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e_end = e_begin + e_count;
+  if ((g << 2) >= e_end) return;
+  const uint64_t ctr = (uint64_t)g + offset;
+  const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+  float n[4];
+  box_muller(w.x, w.y, n[0], n[1]);
+  box_muller(w.z, w.w, n[2], n[3]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t e = (g << 2) + q;
+    if (e >= e_begin && e < e_end) eps[e - e_begin] = n[q];
+  }
+}
+
+__global__ void philox_raw_kernel(uint32_t* out, int64_t n, uint64_t ctr0, uint32_t k0,
+                                  uint32_t k1) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t c = ctr0 + (uint64_t)i;
+  const u32x4 w = philox4x32_10(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0u, 0u}, k0, k1);
+  out[4 * i + 0] = w.x;
+  out[4 * i + 1] = w.y;
+  out[4 * i + 2] = w.z;
+  out[4 * i + 3] = w.w;
+}
+
+// ------------------------------------------------------------- conversions
+template <typename S, typename D>
+__global__ void convert_kernel(const S* __restrict__ src, D* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (D)src[i];
+}
+
+// out[i] = sum_k in[k*n + i], k < nslab (fixed order -> deterministic).
+template <typename D>
+__global__ void sum_slabs_kernel(const float* __restrict__ in, int64_t nslab, int64_t n,
+                                 D* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.0f;
+    for (int64_t k = 0; k < nslab; ++k) acc += in[k * n + i];
+    out[i] = (D)acc;
+  }
+}
+
+// gathered (R,6,B) -> out (6,B)
+__global__ void bstat_combine_kernel(const float* __restrict__ g, int64_t R, int64_t B,
+                                     float* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+#pragma unroll
+  for (int br = 0; br < 2; ++br) {
+    const int mi = 2 * br, zi = 2 * br + 1;
+    float M = -INFINITY;
+    for (int64_t r = 0; r < R; ++r) M = fmaxf(M, g[(r * 6 + mi) * B + b]);
+    float Z = 0.0f;
+    for (int64_t r = 0; r < R; ++r)
+      Z += g[(r * 6 + zi) * B + b] * expf(g[(r * 6 + mi) * B + b] - M);
+    out[mi * B + b] = M;
+    out[zi * B + b] = Z;
+  }
+  for (int k = 4; k < 6; ++k) {
+    float acc = 0.0f;
+    for (int64_t r = 0; r < R; ++r) acc += g[(r * 6 + k) * B + b];
+    out[k * B + b] = acc;
+  }
+}
+
+// ------------------------------------------------------ reparameterisation
+// z = mu + eps * exp(0.5 * logvar)  (mpvae.py:67-69, 72-74), both encoders.
+__global__ void reparam_fwd_kernel(mpv_reparam_args a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.n_e) {
+    a.z_e[i] = a.mu_e[i] + a.eps_e[i] * expf(0.5f * a.logvar_e[i]);
+  } else if (i - a.n_e < a.n_x) {
+    const int64_t j = i - a.n_e;
+    a.z_x[j] = a.mu_x[j] + a.eps_x[j] * expf(0.5f * a.logvar_x[j]);
+  }
+}
+
+__global__ void reparam_bwd_kernel(mpv_reparam_bwd_args a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float* gz;
+  const float* lv;
+  const float* ep;
+  float* gmu;
+  float* glv;
+  int64_t j;
+  if (i < a.n_e) {
+    gz = a.gz_e; lv = a.logvar_e; ep = a.eps_e; gmu = a.gmu_e; glv = a.glogvar_e; j = i;
+  } else if (i - a.n_e < a.n_x) {
+    gz = a.gz_x; lv = a.logvar_x; ep = a.eps_x; gmu = a.gmu_x; glv = a.glogvar_x; j = i - a.n_e;
+  } else {
+    return;
+  }
+  const float g = gz ? gz[j] : 0.0f;
+  gmu[j] = g;
+  glv[j] = g * ep[j] * 0.5f * expf(0.5f * lv[j]);
+}
+
+// d KL / d (mu, logvar) of mpvae.py:147-148, scaled by the upstream gradient
+// g = gscal[KL] + 1.1 * gscal[TOTAL].
+__global__ void kl_bwd_kernel(mpv_kl_bwd_args a) {
+  const int64_t n = a.B * a.d;
+  const float g = a.gscal[MPV_G_KL] + kKlWeight * a.gscal[MPV_G_TOTAL];
+  const float s = 0.5f * g / (float)a.B;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
+    const float dm = a.fx_mu[i] - a.fe_mu[i];
+    const float ex = expf(lvx);
+    const float den = ex + kKlEps;
+    const float r = expf(lve - lvx);
+    const float gm = s * 2.0f * dm / den;
+    a.g_fe_mu[i] = -gm;
+    a.g_fx_mu[i] = gm;
+    a.g_fe_logvar[i] = s * (r - 1.0f);
+    a.g_fx_logvar[i] = s * (1.0f - r - dm * dm * ex / (den * den));
+  }
+}
+
+static unsigned grid_for(int64_t n, int threads, int64_t cap = 65536) {
+  int64_t g = cdiv(n, threads);
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace mpv
+
+using namespace mpv;
+
+extern "C" {
+
+int mpv_abi_version(void) { return MPV_ABI_VERSION; }
+
+int mpv_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing = on != 0;
+  return MPV_OK;
+}
+
+int mpv_timing_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  for (auto& t : g_slots) t.used = 0;
+  return MPV_OK;
+}
+
+int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms) {
+  MPV_REQUIRE(kernel && launches && total_ms, "bad timing_query arguments");
+  std::lock_guard<std::mutex> lk(g_tmu);
+  *launches = 0;
+  *total_ms = 0.0;
+  for (auto& t : g_slots) {
+    if (t.name != kernel) continue;
+    for (size_t i = 0; i < t.used; ++i) {
+      float ms = 0.0f;
+      hipError_t e = hipEventSynchronize(t.stop[i]);
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, t.start[i], t.stop[i]);
+      if (e != hipSuccess) return fail(MPV_ELAUNCH, "timing %s: %s", kernel, hipGetErrorString(e));
+      *total_ms += ms;
+      *launches += 1;
+    }
+  }
+  return MPV_OK;
+}
+
+const char* mpv_last_error(void) { return g_err; }
+
+int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                     void* stream) {
+  if (int rc = check_shape(shape)) return rc;
+  MPV_REQUIRE(eps != nullptr, "eps is NULL");
+  const int64_t per_s = shape->B * shape->z;
+  const int64_t e_begin = shape->s_offset * per_s;
+  const int64_t e_count = shape->S_local * per_s;
+  const int64_t first = e_begin >> 2, last = (e_begin + e_count - 1) >> 2;
+  const int64_t nthreads = last - first + 1;
+  const int threads = 256;
+  const int64_t blocks = cdiv(nthreads, threads);
+  MPV_REQUIRE(blocks < (int64_t(1) << 31), "noise too large");
+  MPV_LAUNCH("noise_philox", noise_philox_kernel, dim3((unsigned)blocks), dim3(threads), 0,
+                     as_stream(stream), eps, e_begin, e_count, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), offset);
+  return check_launch("noise_philox");
+}
+
+int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* stream) {
+  MPV_REQUIRE(out != nullptr && n > 0, "bad philox_raw arguments");
+  MPV_LAUNCH("philox_raw", philox_raw_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), out, n, ctr0, (uint32_t)key, (uint32_t)(key >> 32));
+  return check_launch("philox_raw");
+}
+
+int mpv_convert(const void* src, int sd, void* dst, int dd, int64_t n, void* stream) {
+  MPV_REQUIRE(src && dst && n >= 0, "bad convert arguments");
+  MPV_REQUIRE((sd == MPV_F32 || sd == MPV_F64) && (dd == MPV_F32 || dd == MPV_F64),
+              "unsupported dtype pair %d -> %d", sd, dd);
+  if (n == 0) return MPV_OK;
+  const unsigned g = grid_for(n, 256);
+  hipStream_t s = as_stream(stream);
+  if (sd == MPV_F64 && dd == MPV_F32)
+    MPV_LAUNCH("convert", (convert_kernel<double, float>), dim3(g), dim3(256), 0, s,
+                       (const double*)src, (float*)dst, n);
+  else if (sd == MPV_F32 && dd == MPV_F64)
+    MPV_LAUNCH("convert", (convert_kernel<float, double>), dim3(g), dim3(256), 0, s,
+                       (const float*)src, (double*)dst, n);
+  else if (sd == MPV_F32)
+    MPV_LAUNCH("convert", (convert_kernel<float, float>), dim3(g), dim3(256), 0, s,
+                       (const float*)src, (float*)dst, n);
+  else
+    MPV_LAUNCH("convert", (convert_kernel<double, double>), dim3(g), dim3(256), 0, s,
+                       (const double*)src, (double*)dst, n);
+  return check_launch("convert");
+}
+
+int mpv_bstat_combine(const float* gathered, int64_t nshards, int64_t B, float* out,
+                      void* stream) {
+  MPV_REQUIRE(gathered && out && nshards > 0 && B > 0, "bad bstat_combine arguments");
+  MPV_LAUNCH("bstat_combine", bstat_combine_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0,
+                     as_stream(stream), gathered, nshards, B, out);
+  return check_launch("bstat_combine");
+}
+
+int mpv_reparam_fwd(const mpv_reparam_args* a, void* stream) {
+  MPV_REQUIRE(a != nullptr && a->n_e >= 0 && a->n_x >= 0, "bad reparam arguments");
+  MPV_REQUIRE(a->n_e == 0 || (a->mu_e && a->logvar_e && a->eps_e && a->z_e), "label encoder NULL");
+  MPV_REQUIRE(a->n_x == 0 || (a->mu_x && a->logvar_x && a->eps_x && a->z_x), "feat encoder NULL");
+  const int64_t n = a->n_e + a->n_x;
+  if (n == 0) return MPV_OK;
+  MPV_LAUNCH("reparam_fwd", reparam_fwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), *a);
+  return check_launch("reparam_fwd");
+}
+
+int mpv_reparam_bwd(const mpv_reparam_bwd_args* a, void* stream) {
+  MPV_REQUIRE(a != nullptr && a->n_e >= 0 && a->n_x >= 0, "bad reparam_bwd arguments");
+  MPV_REQUIRE(a->n_e == 0 || (a->logvar_e && a->eps_e && a->gmu_e && a->glogvar_e),
+              "label encoder NULL");
+  MPV_REQUIRE(a->n_x == 0 || (a->logvar_x && a->eps_x && a->gmu_x && a->glogvar_x),
+              "feat encoder NULL");
+  const int64_t n = a->n_e + a->n_x;
+  if (n == 0) return MPV_OK;
+  MPV_LAUNCH("reparam_bwd", reparam_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), *a);
+  return check_launch("reparam_bwd");
+}
+
+int mpv_kl_bwd(const mpv_kl_bwd_args* a, void* stream) {
+  MPV_REQUIRE(a && a->fe_mu && a->fe_logvar && a->fx_mu && a->fx_logvar && a->gscal &&
+                  a->g_fe_mu && a->g_fe_logvar && a->g_fx_mu && a->g_fx_logvar,
+              "bad kl_bwd arguments");
+  MPV_REQUIRE(a->B > 0 && a->d > 0, "bad kl_bwd sizes");
+  MPV_LAUNCH("kl_bwd", kl_bwd_kernel, dim3(grid_for(a->B * a->d, 256, 4096)), dim3(256), 0,
+                     as_stream(stream), *a);
+  return check_launch("kl_bwd");
+}
+
+}  // extern "C"
+
+namespace mpv {
+// Used by the forward / backward translation units.
+int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
+                     hipStream_t s) {
+  const unsigned g = grid_for(n, 256, 8192);
+  if (out_dtype == MPV_F64)
+    MPV_LAUNCH("sum_slabs", (sum_slabs_kernel<double>), dim3(g), dim3(256), 0, s, in, nslab, n,
+                       (double*)out);
+  else
+    MPV_LAUNCH("sum_slabs", (sum_slabs_kernel<float>), dim3(g), dim3(256), 0, s, in, nslab, n,
+                       (float*)out);
+  return check_launch("sum_slabs");
+}
+}  // namespace mpv

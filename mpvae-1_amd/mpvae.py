@@ -1,0 +1,176 @@
+"""Drop-in replacement of reference ``mpvae.py`` (lliutianc/MPVAE-1) on MI355X.
+
+Same public names, signatures, parameter names, shapes and dtypes:
+
+  VAE(args)                       nn.Module, reference mpvae.py:10-100
+  compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
+               r_sqrt_sigma, args) -> (total, nll, nll_x, c, c_x, kl,
+                                       indiv_prob, indiv_prob_label)
+                                  reference mpvae.py:145-210
+
+Put ``mpvae-1_amd/`` on ``sys.path`` and ``from mpvae import VAE, compute_loss``
+works unchanged in the reference's training loop (fairsoft_train.py:57-146).
+The arithmetic runs in hand-written gfx950 kernels (libmpvae_hip.so); the
+encoder/decoder MLPs stay ``nn.Linear`` (hipBLASLt), as SURVEY.md section 8(a)
+rows a2/a4 prescribe.
+
+Build-only knobs read from ``args`` (defaults reproduce the reference):
+  mpvae_noise  "torch_cpu" (default): draw the probit noise from torch's CPU
+               default generator exactly as mpvae.py:162 does (same values,
+               same RNG consumption), then copy it to the device;
+               "philox": generate it on the device with the counter-based
+               Philox4x32-10 kernel (perf mode; a different, equally
+               distributed N(0,1) stream -- DESIGN.md);
+               a (n_sample, B, z_dim) float32 tensor: use it as the noise.
+  mpvae_seed   philox seed (default: drawn from torch's CPU generator, so
+               runs are reproducible under torch.manual_seed).
+  mpvae_shard  True: shard the n_sample axis over the default
+               torch.distributed group (mpvae_dist.py); default False.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import mpvae_hip
+import mpvae_dist
+from mpvae_ops import ElboConfig, FusedReparam, ProbitELBO, SingleReparam
+
+__all__ = ["VAE", "compute_loss"]
+
+# (attribute, in_features, out_features) in the reference's construction order
+# (mpvae.py:14-32).  The order fixes the torch init draws and the state_dict
+# key order, so seeded runs and existing .pkl checkpoints carry over.
+def _layer_table(F_, d, L):
+    return [
+        ("fx1", F_, 256), ("fx2", 256, 512), ("fx3", 512, 256),
+        ("fx_mu", 256, d), ("fx_logvar", 256, d),
+        ("fd_x1", F_ + d, 256), ("fd_x2", 256, 512), ("feat_mp_mu", 512, L),
+        ("fe1", F_ + L, 512), ("fe2", 512, 256),
+        ("fe_mu", 256, d), ("fe_logvar", 256, d),
+    ]
+
+
+def _init_r_sqrt_sigma(args):
+    """r_sqrt_sigma (L, z): mpvae.py:40-48.  'random' -> fp64 frozen,
+    'zero' -> fp32 zeros frozen, otherwise fp64 trainable; uniform draws come
+    from numpy's global RNG like the reference."""
+    L, z = args.label_dim, args.z_dim
+    bound = np.sqrt(6.0 / (L + z))
+    if args.residue_sigma == "zero":
+        return nn.Parameter(torch.zeros((L, z)), requires_grad=False)
+    draw = torch.from_numpy(np.random.uniform(-bound, bound, (L, z)))
+    return nn.Parameter(draw, requires_grad=args.residue_sigma != "random")
+
+
+class VAE(nn.Module):
+    """MPVAE: label encoder q(z|x,y), feature encoder p(z|x), shared decoder."""
+
+    def __init__(self, args):
+        super().__init__()
+        for name, n_in, n_out in _layer_table(args.feature_dim, args.latent_dim, args.label_dim):
+            setattr(self, name, nn.Linear(n_in, n_out))
+        # the label branch decodes through the feature branch's first two layers
+        self.fd1 = self.fd_x1
+        self.fd2 = self.fd_x2
+        self.label_mp_mu = nn.Linear(512, args.label_dim)
+        assert self.fd1 is self.fd_x1 and self.fd2 is self.fd_x2
+        self.dropout = nn.Dropout(p=args.keep_prob)   # keep_prob is the DROP rate (mpvae.py:38)
+        self.scale_coeff = args.scale_coeff
+        self.register_parameter("r_sqrt_sigma", _init_r_sqrt_sigma(args))
+        # eps ~ N(0,1) like torch.randn_like (mpvae.py:68,73); replaceable for tests
+        self.reparam_noise = torch.randn_like
+
+    # -- encoders (mpvae.py:51-64)
+    def _mlp(self, x, layers):
+        for lin in layers:
+            x = self.dropout(F.relu(lin(x)))
+        return x
+
+    def label_encode(self, x):
+        h = self._mlp(x, (self.fe1, self.fe2))
+        return self.fe_mu(h) * self.scale_coeff, self.fe_logvar(h) * self.scale_coeff
+
+    def feat_encode(self, x):
+        h = self._mlp(x, (self.fx1, self.fx2, self.fx3))
+        return self.fx_mu(h) * self.scale_coeff, self.fx_logvar(h) * self.scale_coeff
+
+    # -- reparameterisation (mpvae.py:66-74), one encoder at a time
+    def label_reparameterize(self, mu, logvar):
+        return SingleReparam.apply(mu, logvar, self.reparam_noise(logvar))
+
+    def feat_reparameterize(self, mu, logvar):
+        return SingleReparam.apply(mu, logvar, self.reparam_noise(logvar))
+
+    # -- decoders (mpvae.py:76-84); fd1/fd2 are fd_x1/fd_x2
+    def _decode(self, z, head):
+        return head(F.relu(self.fd_x2(F.relu(self.fd_x1(z)))))
+
+    def label_decode(self, z):
+        return self._decode(z, self.label_mp_mu)
+
+    def feat_decode(self, z):
+        return self._decode(z, self.feat_mp_mu)
+
+    def label_forward(self, x, feat):
+        mu, logvar = self.label_encode(torch.cat((feat, x), 1))
+        z = self.label_reparameterize(mu, logvar)
+        return self.label_decode(torch.cat((feat, z), 1)), mu, logvar
+
+    def feat_forward(self, x):
+        mu, logvar = self.feat_encode(x)
+        z = self.feat_reparameterize(mu, logvar)
+        return self.feat_decode(torch.cat((x, z), 1)), mu, logvar
+
+    def forward(self, label, feature):
+        """(label_out, label_mu, label_logvar, feat_out, feat_mu, feat_logvar).
+
+        Both encoders are evaluated first and reparameterised by ONE fused
+        launch.  RNG draws keep the reference order: label-encoder dropouts,
+        label eps, feature-encoder dropouts, feature eps (mpvae.py:86-100)."""
+        mu_e, lv_e = self.label_encode(torch.cat((feature, label), 1))
+        eps_e = self.reparam_noise(lv_e)
+        mu_x, lv_x = self.feat_encode(feature)
+        eps_x = self.reparam_noise(lv_x)
+        z_e, z_x = FusedReparam.apply(mu_e, lv_e, eps_e, mu_x, lv_x, eps_x)
+        label_out = self.label_decode(torch.cat((feature, z_e), 1))
+        feat_out = self.feat_decode(torch.cat((feature, z_x), 1))
+        return label_out, mu_e, lv_e, feat_out, mu_x, lv_x
+
+
+def _noise_source(args, n_sample, B, z, shard, device):
+    """(noise tensor or None, ElboConfig kwargs) for compute_loss."""
+    mode = getattr(args, "mpvae_noise", "torch_cpu")
+    s0, s1 = shard.s_offset, shard.s_offset + shard.S_local
+    if isinstance(mode, torch.Tensor):
+        if tuple(mode.shape) != (n_sample, B, z):
+            raise ValueError(f"args.mpvae_noise must be {(n_sample, B, z)}, got {tuple(mode.shape)}")
+        return mode[s0:s1].to(device=device, dtype=torch.float32), dict(noise="explicit")
+    if mode == "torch_cpu":
+        # mpvae.py:162 -- same generator, same draw, same shape; then H2D
+        noise = torch.normal(0, 1, size=(n_sample, B, z))
+        return noise[s0:s1].to(device), dict(noise="explicit")
+    if mode == "philox":
+        seed = getattr(args, "mpvae_seed", None)
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return None, dict(noise="philox", seed=seed, offset=0)
+    raise ValueError(f"unknown args.mpvae_noise {mode!r} (torch_cpu | philox | tensor)")
+
+
+def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
+                 r_sqrt_sigma, args):
+    """Multivariate-probit ELBO of reference mpvae.py:145-210 (8-tuple)."""
+    mpvae_hip.require_gpu(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
+                          r_sqrt_sigma)
+    n_sample = args.n_train_sample if args.mode == "train" else args.n_test_sample
+    B, z = fe_out.shape[0], args.z_dim
+    if r_sqrt_sigma.dim() != 2 or r_sqrt_sigma.shape[1] != z:
+        raise ValueError(f"r_sqrt_sigma must be (label_dim, z_dim={z}), "
+                         f"got {tuple(r_sqrt_sigma.shape)}")
+    shard = mpvae_dist.shard_for(args, n_sample)
+    noise, kw = _noise_source(args, n_sample, B, z, shard, fe_out.device)
+    cfg = ElboConfig(n_sample, shard.S_local, shard.s_offset, args.nll_coeff, args.c_coeff,
+                     exchange=shard.exchange, **kw)
+    return ProbitELBO.apply(input_label.float(), fe_out, fe_mu, fe_logvar, fx_out, fx_mu,
+                            fx_logvar, r_sqrt_sigma, noise, cfg)

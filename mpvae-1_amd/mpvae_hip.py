@@ -1,0 +1,157 @@
+"""ctypes binding of libmpvae_hip.so (C ABI: include/mpvae_hip.h).
+
+The library is loaded from this directory, after ``import torch`` so that the
+HIP runtime torch already loaded is the one the kernels register with (both
+share the SONAME libamdhip64.so.7).  There is deliberately no fallback: if the
+library is missing or the device is not a GPU, every entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the .so load: one HIP runtime per process)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
+
+ABI_VERSION = 1
+F32, F64 = 0, 1
+G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+vp = ctypes.c_void_p
+
+
+class MPVError(RuntimeError):
+    """An MPV_E* status returned by libmpvae_hip.so."""
+
+
+class Shape(ctypes.Structure):
+    _fields_ = [("S_local", ctypes.c_int64), ("S_total", ctypes.c_int64),
+                ("s_offset", ctypes.c_int64), ("B", ctypes.c_int64), ("L", ctypes.c_int64),
+                ("z", ctypes.c_int64)]
+
+
+class FwdArgs(ctypes.Structure):
+    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("R32", vp), ("eps", vp), ("T", vp),
+                ("rowstat", vp), ("bstat", vp), ("colsum", vp), ("workspace", vp),
+                ("workspace_bytes", ctypes.c_size_t)]
+
+
+class FinalArgs(ctypes.Structure):
+    _fields_ = [("bstat", vp), ("colsum", vp), ("fe_mu", vp), ("fe_logvar", vp), ("fx_mu", vp),
+                ("fx_logvar", vp), ("d", ctypes.c_int64), ("nll_coeff", ctypes.c_float),
+                ("c_coeff", ctypes.c_float), ("total", vp), ("nll", vp), ("nll_x", vp),
+                ("c", vp), ("c_x", vp), ("kl", vp), ("indiv_prob", vp),
+                ("indiv_prob_label", vp)]
+
+
+class BwdArgs(ctypes.Structure):
+    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("eps", vp), ("T", vp),
+                ("rowstat", vp), ("bstat", vp), ("gscal", vp), ("g_indiv", vp),
+                ("g_indiv_label", vp), ("nll_coeff", ctypes.c_float),
+                ("c_coeff", ctypes.c_float), ("live", ctypes.c_int), ("dfe_dfx", vp),
+                ("dR32", vp), ("workspace", vp), ("workspace_bytes", ctypes.c_size_t)]
+
+
+class KlBwdArgs(ctypes.Structure):
+    _fields_ = [("fe_mu", vp), ("fe_logvar", vp), ("fx_mu", vp), ("fx_logvar", vp),
+                ("B", ctypes.c_int64), ("d", ctypes.c_int64), ("gscal", vp), ("g_fe_mu", vp),
+                ("g_fe_logvar", vp), ("g_fx_mu", vp), ("g_fx_logvar", vp)]
+
+
+class ReparamArgs(ctypes.Structure):
+    _fields_ = [("mu_e", vp), ("logvar_e", vp), ("eps_e", vp), ("z_e", vp), ("n_e", ctypes.c_int64),
+                ("mu_x", vp), ("logvar_x", vp), ("eps_x", vp), ("z_x", vp), ("n_x", ctypes.c_int64)]
+
+
+class ReparamBwdArgs(ctypes.Structure):
+    _fields_ = [("gz_e", vp), ("logvar_e", vp), ("eps_e", vp), ("gmu_e", vp), ("glogvar_e", vp),
+                ("n_e", ctypes.c_int64), ("gz_x", vp), ("logvar_x", vp), ("eps_x", vp),
+                ("gmu_x", vp), ("glogvar_x", vp), ("n_x", ctypes.c_int64)]
+
+
+# name -> (restype, argtypes); exactly the symbols of include/mpvae_hip.h
+SIGNATURES = {
+    "mpv_abi_version": (ctypes.c_int, []),
+    "mpv_last_error": (ctypes.c_char_p, []),
+    "mpv_noise_philox": (ctypes.c_int, [vp, ctypes.POINTER(Shape), ctypes.c_uint64,
+                                        ctypes.c_uint64, vp]),
+    "mpv_philox_raw": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mpv_convert": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int64, vp]),
+    "mpv_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
+    "mpv_probit_fwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FwdArgs), vp]),
+    "mpv_bstat_combine": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int64, vp, vp]),
+    "mpv_probit_finalize": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FinalArgs), vp]),
+    "mpv_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
+    "mpv_probit_bwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(BwdArgs), vp]),
+    "mpv_kl_bwd": (ctypes.c_int, [ctypes.POINTER(KlBwdArgs), vp]),
+    "mpv_reparam_fwd": (ctypes.c_int, [ctypes.POINTER(ReparamArgs), vp]),
+    "mpv_reparam_bwd": (ctypes.c_int, [ctypes.POINTER(ReparamBwdArgs), vp]),
+    "mpv_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "mpv_timing_reset": (ctypes.c_int, []),
+    "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_double)]),
+}
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load (once) and type the C ABI.  Raises if the library is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise MPVError(f"libmpvae_hip.so not found at {p}: run `make -C mpvae-1_amd` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.mpv_abi_version() != ABI_VERSION:
+        raise MPVError(f"ABI mismatch: library {lib.mpv_abi_version()} != {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load_library().mpv_last_error().decode(errors="replace")
+        raise MPVError(f"{what} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(*tensors):
+    """The product path runs only on the GPU; CPU tensors are an error, not a fallback."""
+    for t in tensors:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError("mpvae-1_amd runs the probit-ELBO hot path on the GPU only "
+                               f"(got a {t.device} tensor); move inputs to a ROCm device")
+    load_library()
+
+
+KERNELS = ["noise_philox", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
+           "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
+           "kl_bwd"]
+
+
+def kernel_times():
+    """{kernel: (launches, total_ms)} recorded since the last mpv_timing_reset()."""
+    lib = load_library()
+    out = {}
+    for k in KERNELS:
+        n, ms = ctypes.c_int64(), ctypes.c_double()
+        check(lib.mpv_timing_query(k.encode(), ctypes.byref(n), ctypes.byref(ms)), "timing_query")
+        if n.value:
+            out[k] = (n.value, ms.value)
+    return out

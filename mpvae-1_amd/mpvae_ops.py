@@ -1,0 +1,267 @@
+"""Autograd Functions over the HIP kernels of libmpvae_hip.so.
+
+``ProbitELBO`` is the whole of reference ``compute_loss`` (mpvae.py:145-210) as
+one custom Function: its forward launches noise (optional) -> fused GEMM +
+probit decode + row statistics -> combine -> finalize, and its backward the
+analytic gradient kernels.  Sharding of the
+Monte-Carlo axis across ranks plugs in through ``exchange`` (mpvae_dist.py);
+the per-shard arithmetic through ``backend`` (``HipShardBackend`` here -- the
+only backend the product ever uses).
+
+``FusedReparam`` is the reparameterisation of both encoders in one launch
+(mpvae.py:66-74).
+"""
+import torch
+
+import mpvae_hip as H
+
+
+def _f32(t, name):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+class HipShardBackend:
+    """Per-shard arithmetic on the GPU through the C ABI."""
+
+    def shape(self, S_local, S_total, s_offset, B, L, z):
+        return H.Shape(S_local, S_total, s_offset, B, L, z)
+
+    def make_noise(self, shape, device, seed, offset):
+        eps = torch.empty((shape.S_local, shape.B, shape.z), device=device, dtype=torch.float32)
+        H.check(H.load_library().mpv_noise_philox(H.ptr(eps), shape, seed, offset,
+                                                  H.stream_of(device)), "mpv_noise_philox")
+        return eps
+
+    def to_f32(self, R):
+        if R.dtype == torch.float32:
+            return R.contiguous()
+        if R.dtype != torch.float64:
+            raise TypeError(f"r_sqrt_sigma must be float32 or float64 (got {R.dtype})")
+        R = R.contiguous()
+        out = torch.empty(R.shape, device=R.device, dtype=torch.float32)
+        H.check(H.load_library().mpv_convert(H.ptr(R), H.F64, H.ptr(out), H.F32, R.numel(),
+                                             H.stream_of(R.device)), "mpv_convert")
+        return out
+
+    def from_f32(self, x32, dtype):
+        if dtype == torch.float32:
+            return x32
+        out = torch.empty(x32.shape, device=x32.device, dtype=dtype)
+        H.check(H.load_library().mpv_convert(H.ptr(x32), H.F32, H.ptr(out), H.F64, x32.numel(),
+                                             H.stream_of(x32.device)), "mpv_convert")
+        return out
+
+    def forward_local(self, shape, y, fe_out, fx_out, R32, eps, keep_T):
+        lib = H.load_library()
+        dev = y.device
+        S, B, L = shape.S_local, shape.B, shape.L
+        T = torch.empty((B, S, L), device=dev, dtype=torch.float32) if keep_T else None
+        rowstat = torch.empty((6, B, S), device=dev, dtype=torch.float32)
+        bstat = torch.empty((6, B), device=dev, dtype=torch.float32)
+        colsum = torch.empty((2, B, L), device=dev, dtype=torch.float32)
+        nbytes = lib.mpv_fwd_workspace_bytes(shape)
+        ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
+        args = H.FwdArgs(H.ptr(y), H.ptr(fe_out), H.ptr(fx_out), H.ptr(R32), H.ptr(eps), H.ptr(T),
+                         H.ptr(rowstat), H.ptr(bstat), H.ptr(colsum), H.ptr(ws), nbytes)
+        H.check(lib.mpv_probit_fwd(shape, args, H.stream_of(dev)), "mpv_probit_fwd")
+        return dict(rowstat=rowstat, bstat=bstat, colsum=colsum, T=T)
+
+    def combine_bstats(self, gathered):
+        R, _, B = gathered.shape
+        out = torch.empty((6, B), device=gathered.device, dtype=torch.float32)
+        H.check(H.load_library().mpv_bstat_combine(H.ptr(gathered.contiguous()), R, B, H.ptr(out),
+                                                   H.stream_of(gathered.device)),
+                "mpv_bstat_combine")
+        return out
+
+    def finalize(self, shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar, nll_coeff,
+                 c_coeff):
+        dev = bstat.device
+        B, L = shape.B, shape.L
+        scal = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(6)]
+        indiv = torch.empty((B, L), device=dev, dtype=torch.float32)
+        indiv_label = torch.empty((B, L), device=dev, dtype=torch.float32)
+        args = H.FinalArgs(H.ptr(bstat), H.ptr(colsum), H.ptr(fe_mu), H.ptr(fe_logvar),
+                           H.ptr(fx_mu), H.ptr(fx_logvar), fe_mu.shape[1], nll_coeff, c_coeff,
+                           *[H.ptr(s) for s in scal], H.ptr(indiv), H.ptr(indiv_label))
+        H.check(H.load_library().mpv_probit_finalize(shape, args, H.stream_of(dev)),
+                "mpv_probit_finalize")
+        return (*scal, indiv, indiv_label)
+
+    def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR):
+        lib = H.load_library()
+        dev = gscal.device
+        B, L, z = shape.B, shape.L, shape.z
+        n_fe = 2 * B * L
+        flat = torch.empty((n_fe + (L * z if want_dR else 0),), device=dev, dtype=torch.float32)
+        dfe_dfx = flat[:n_fe].view(2, B, L)
+        dR32 = flat[n_fe:].view(L, z) if want_dR else None
+        nbytes = lib.mpv_bwd_workspace_bytes(shape)
+        ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
+        args = H.BwdArgs(H.ptr(saved["y"]), H.ptr(saved["fe_out"]), H.ptr(saved["fx_out"]),
+                         H.ptr(saved["eps"]), H.ptr(saved["T"]), H.ptr(saved["rowstat"]),
+                         H.ptr(saved["bstat"]), H.ptr(gscal), H.ptr(g_I), H.ptr(g_IL),
+                         nll_coeff, c_coeff, live, H.ptr(dfe_dfx), H.ptr(dR32), H.ptr(ws), nbytes)
+        H.check(lib.mpv_probit_bwd(shape, args, H.stream_of(dev)), "mpv_probit_bwd")
+        return flat, dfe_dfx, dR32
+
+    def kl_backward(self, fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
+        B, d = fe_mu.shape
+        outs = [torch.empty_like(fe_mu) for _ in range(4)]
+        args = H.KlBwdArgs(H.ptr(fe_mu), H.ptr(fe_logvar), H.ptr(fx_mu), H.ptr(fx_logvar), B, d,
+                           H.ptr(gscal), *[H.ptr(o) for o in outs])
+        H.check(H.load_library().mpv_kl_bwd(args, H.stream_of(fe_mu.device)), "mpv_kl_bwd")
+        return outs  # g_fe_mu, g_fe_logvar, g_fx_mu, g_fx_logvar
+
+
+class LocalExchange:
+    """Single shard: global statistics are the local ones."""
+    world = 1
+
+    def combine(self, bstat, colsum, backend):
+        return bstat, colsum
+
+    def reduce_grads(self, flat):
+        return flat
+
+
+class ElboConfig:
+    """Non-tensor arguments of ProbitELBO."""
+
+    def __init__(self, S_total, S_local, s_offset, nll_coeff, c_coeff, noise="explicit",
+                 seed=0, offset=0, backend=None, exchange=None):
+        self.S_total, self.S_local, self.s_offset = int(S_total), int(S_local), int(s_offset)
+        self.nll_coeff, self.c_coeff = float(nll_coeff), float(c_coeff)
+        self.noise, self.seed, self.offset = noise, int(seed), int(offset)
+        self.backend = backend if backend is not None else HipShardBackend()
+        self.exchange = exchange if exchange is not None else LocalExchange()
+
+
+class ProbitELBO(torch.autograd.Function):
+    """(total, nll, nll_x, c, c_x, kl, indiv_prob, indiv_prob_label) of mpvae.py:145-210."""
+
+    @staticmethod
+    def forward(ctx, y, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar, R, eps, cfg):
+        be = cfg.backend
+        y, fe_out, fx_out = _f32(y, "input_label"), _f32(fe_out, "fe_out"), _f32(fx_out, "fx_out")
+        fe_mu, fe_logvar = _f32(fe_mu, "fe_mu"), _f32(fe_logvar, "fe_logvar")
+        fx_mu, fx_logvar = _f32(fx_mu, "fx_mu"), _f32(fx_logvar, "fx_logvar")
+        B, L = y.shape
+        if fe_out.shape != (B, L) or fx_out.shape != (B, L):
+            raise ValueError(f"fe_out/fx_out must be {(B, L)}, got {tuple(fe_out.shape)}, "
+                             f"{tuple(fx_out.shape)}")
+        if R.dim() != 2 or R.shape[0] != L:
+            raise ValueError(f"r_sqrt_sigma must be (label_dim={L}, z_dim), got {tuple(R.shape)}")
+        z = R.shape[1]
+        shape = be.shape(cfg.S_local, cfg.S_total, cfg.s_offset, B, L, z)
+        if cfg.noise == "philox":
+            eps = be.make_noise(shape, y.device, cfg.seed, cfg.offset)
+        else:
+            eps = _f32(eps, "noise")
+            if tuple(eps.shape) != (cfg.S_local, B, z):
+                raise ValueError(f"noise must be {(cfg.S_local, B, z)}, got {tuple(eps.shape)}")
+        R32 = be.to_f32(R)
+        need = ctx.needs_input_grad
+        keep_T = need[1] or need[4] or need[7]
+        loc = be.forward_local(shape, y, fe_out, fx_out, R32, eps, keep_T)
+        bstat, colsum = cfg.exchange.combine(loc["bstat"], loc["colsum"], be)
+        outs = be.finalize(shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
+                           cfg.nll_coeff, cfg.c_coeff)
+        ctx.set_materialize_grads(False)
+        ctx.cfg, ctx.shape, ctx.r_dtype, ctx.keep_T = cfg, shape, R.dtype, keep_T
+        ctx.consumed = False
+        if any(need[:8]):
+            ctx.saved = dict(y=y, fe_out=fe_out, fx_out=fx_out, eps=eps, T=loc["T"],
+                             rowstat=loc["rowstat"], bstat=bstat, fe_mu=fe_mu,
+                             fe_logvar=fe_logvar, fx_mu=fx_mu, fx_logvar=fx_logvar)
+        return outs
+
+    @staticmethod
+    def backward(ctx, g_total, g_nll, g_nll_x, g_c, g_c_x, g_kl, g_I, g_IL):
+        if ctx.consumed:
+            raise RuntimeError("ProbitELBO backward reuses its forward buffers in place; "
+                               "backward through the same compute_loss twice is not supported")
+        ctx.consumed = True
+        cfg, shape, be, sv = ctx.cfg, ctx.shape, ctx.cfg.backend, ctx.saved
+        need = ctx.needs_input_grad
+        gs = [g_total, g_nll, g_nll_x, g_c, g_c_x, g_kl]
+        live = sum(1 << i for i, g in enumerate(gs) if g is not None)
+        dev = sv["y"].device
+        zero = torch.zeros((), device=dev, dtype=torch.float32)
+        gscal = torch.stack([zero if g is None else g.reshape(()).to(torch.float32) for g in gs])
+        g_I = None if g_I is None else g_I.to(torch.float32).contiguous()
+        g_IL = None if g_IL is None else g_IL.to(torch.float32).contiguous()
+        grads = [None] * 10
+        if ctx.keep_T and (need[1] or need[4] or need[7]):
+            flat, dfe_dfx, dR32 = be.backward_local(shape, sv, gscal, live, g_I, g_IL,
+                                                    cfg.nll_coeff, cfg.c_coeff, need[7])
+            cfg.exchange.reduce_grads(flat)
+            if need[1]:
+                grads[1] = dfe_dfx[0]
+            if need[4]:
+                grads[4] = dfe_dfx[1]
+            if need[7]:
+                grads[7] = be.from_f32(dR32, ctx.r_dtype)
+        if need[2] or need[3] or need[5] or need[6]:
+            gk = be.kl_backward(sv["fe_mu"], sv["fe_logvar"], sv["fx_mu"], sv["fx_logvar"], gscal)
+            grads[2], grads[3], grads[5], grads[6] = gk
+        ctx.saved = None
+        return tuple(grads)
+
+
+class FusedReparam(torch.autograd.Function):
+    """z = mu + eps*exp(0.5*logvar) for the label and the feature encoder in one
+    launch (mpvae.py:66-74).  eps is an input (drawn by the caller with
+    torch.randn_like, so the RNG stream matches the reference's draw order)."""
+
+    @staticmethod
+    def forward(ctx, mu_e, lv_e, eps_e, mu_x, lv_x, eps_x):
+        H.require_gpu(mu_e, mu_x)
+        mu_e, lv_e, eps_e = (_f32(t, "reparam input") for t in (mu_e, lv_e, eps_e))
+        mu_x, lv_x, eps_x = (_f32(t, "reparam input") for t in (mu_x, lv_x, eps_x))
+        z_e, z_x = torch.empty_like(mu_e), torch.empty_like(mu_x)
+        a = H.ReparamArgs(H.ptr(mu_e), H.ptr(lv_e), H.ptr(eps_e), H.ptr(z_e), mu_e.numel(),
+                          H.ptr(mu_x), H.ptr(lv_x), H.ptr(eps_x), H.ptr(z_x), mu_x.numel())
+        H.check(H.load_library().mpv_reparam_fwd(a, H.stream_of(mu_e.device)), "mpv_reparam_fwd")
+        ctx.save_for_backward(lv_e, eps_e, lv_x, eps_x)
+        ctx.set_materialize_grads(False)
+        return z_e, z_x
+
+    @staticmethod
+    def backward(ctx, gz_e, gz_x):
+        lv_e, eps_e, lv_x, eps_x = ctx.saved_tensors
+        gmu_e, glv_e = torch.empty_like(lv_e), torch.empty_like(lv_e)
+        gmu_x, glv_x = torch.empty_like(lv_x), torch.empty_like(lv_x)
+        gz_e = None if gz_e is None else gz_e.contiguous()
+        gz_x = None if gz_x is None else gz_x.contiguous()
+        a = H.ReparamBwdArgs(H.ptr(gz_e), H.ptr(lv_e), H.ptr(eps_e), H.ptr(gmu_e), H.ptr(glv_e),
+                             lv_e.numel(), H.ptr(gz_x), H.ptr(lv_x), H.ptr(eps_x), H.ptr(gmu_x),
+                             H.ptr(glv_x), lv_x.numel())
+        H.check(H.load_library().mpv_reparam_bwd(a, H.stream_of(lv_e.device)), "mpv_reparam_bwd")
+        return gmu_e, glv_e, None, gmu_x, glv_x, None
+
+
+class SingleReparam(torch.autograd.Function):
+    """One encoder's reparameterisation (label_reparameterize / feat_reparameterize)."""
+
+    @staticmethod
+    def forward(ctx, mu, lv, eps):
+        H.require_gpu(mu)
+        mu, lv, eps = (_f32(t, "reparam input") for t in (mu, lv, eps))
+        z = torch.empty_like(mu)
+        a = H.ReparamArgs(H.ptr(mu), H.ptr(lv), H.ptr(eps), H.ptr(z), mu.numel(),
+                          None, None, None, None, 0)
+        H.check(H.load_library().mpv_reparam_fwd(a, H.stream_of(mu.device)), "mpv_reparam_fwd")
+        ctx.save_for_backward(lv, eps)
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        lv, eps = ctx.saved_tensors
+        gmu, glv = torch.empty_like(lv), torch.empty_like(lv)
+        a = H.ReparamBwdArgs(H.ptr(gz.contiguous()), H.ptr(lv), H.ptr(eps), H.ptr(gmu),
+                             H.ptr(glv), lv.numel(), None, None, None, None, None, 0)
+        H.check(H.load_library().mpv_reparam_bwd(a, H.stream_of(lv.device)), "mpv_reparam_bwd")
+        return gmu, glv, None

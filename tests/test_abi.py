@@ -1,0 +1,73 @@
+"""The C ABI library loads and exports exactly what include/mpvae_hip.h declares
+(no GPU needed: only host-side entry points are called)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import mpvae_hip as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mpvae_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpv_[a-z0-9_]+)\s*\(", src)) - {"mpv_shape"})
+
+
+def test_header_declares_the_binding_table():
+    assert declared_functions() == sorted(H.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = H.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", H.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (mpv_\w+)", out))
+    assert exported == set(declared_functions())
+
+
+def test_abi_version_and_host_entry_points():
+    lib = H.load_library()
+    assert lib.mpv_abi_version() == H.ABI_VERSION
+    s = H.Shape(4096, 4096, 0, 512, 1024, 1024)
+    fw, bw = lib.mpv_fwd_workspace_bytes(s), lib.mpv_bwd_workspace_bytes(s)
+    assert 0 < fw < 1 << 30 and 0 < bw < 1 << 30
+    # invalid shapes are rejected on the host, before any launch
+    bad = H.Shape(0, 10, 0, 4, 8, 8)
+    assert lib.mpv_fwd_workspace_bytes(bad) == 0
+    args = H.FwdArgs()
+    assert lib.mpv_probit_fwd(bad, args, None) == 1
+    assert b"sample range" in lib.mpv_last_error()
+    assert lib.mpv_probit_fwd(H.Shape(4, 4, 0, 2, 8, 8), args, None) == 1
+    assert b"NULL" in lib.mpv_last_error()
+    assert lib.mpv_convert(None, 0, None, 0, 4, None) == 1
+
+
+def test_check_raises_with_message():
+    with pytest.raises(H.MPVError, match="NULL"):
+        H.check(H.load_library().mpv_probit_bwd(H.Shape(4, 4, 0, 2, 8, 8), H.BwdArgs(), None),
+                "mpv_probit_bwd")
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+    import mpvae
+    from golden_io import fixtures
+    f = fixtures()[0]
+    t = {k: torch.from_numpy(f[k]) for k in ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out",
+                                              "fx_mu", "fx_logvar", "r_sqrt_sigma"]}
+    with pytest.raises(RuntimeError, match="GPU only"):
+        mpvae.compute_loss(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
+                           t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], f.args())
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(H.MPVError, match="not found"):
+        H.load_library(str(tmp_path / "nope.so"))

@@ -1,0 +1,241 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+vectors and the CPU oracle.  Run with ``pytest -m gpu`` on an MI355X."""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+import mpvae
+import mpvae_hip as H
+from mpvae_ops import ElboConfig, HipShardBackend, ProbitELBO
+from golden_io import DIFF, OUTS, PART_KEYS, fixtures
+from oracle import philox, probit_elbo as pe
+from tolerances import EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL, rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+FIX = fixtures()
+
+
+def _inputs(f, grads=True):
+    t = {k: torch.from_numpy(f[k].copy()).to(DEV) for k in
+         ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar", "r_sqrt_sigma"]}
+    if grads and f.mode == "train":
+        for k in DIFF:
+            t[k].requires_grad_(True)
+        if f.trainable_r:
+            t["r_sqrt_sigma"].requires_grad_(True)
+    return t
+
+
+def _call(t, args):
+    return mpvae.compute_loss(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
+                              t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], args)
+
+
+def _np(x):
+    return x.detach().cpu().double().numpy()
+
+
+@pytest.mark.parametrize("f", FIX, ids=[f.name for f in FIX])
+@pytest.mark.parametrize("kind", ["gtot", "gpart"])
+def test_golden_forward_and_gradients(f, kind):
+    t = _inputs(f)
+    noise = torch.from_numpy(f["noise"])
+    out = _call(t, f.args(mpvae_noise=noise))
+    ftol = EXTREME_FWD_RTOL if f.extreme else FWD_RTOL
+    for k, o in zip(OUTS, out):
+        e = rel_err(_np(o), f["out_" + k])
+        assert e <= ftol, (k, e)
+    if f.mode != "train":
+        return
+    if kind == "gtot":
+        obj = out[0] + (out[6] * torch.from_numpy(f["g_I"]).to(DEV)).sum() + \
+            (out[7] * torch.from_numpy(f["g_IL"]).to(DEV)).sum()
+    else:
+        obj = sum(float(a) * o for a, o in zip(f["a_parts"], out[1:6]))
+    obj.backward()
+    gtol = EXTREME_GRAD_RTOL if f.extreme else GRAD_RTOL
+    for k, v in f.grads(kind).items():
+        g = _np(t[k].grad)
+        assert t[k].grad.dtype == t[k].dtype, k
+        assert np.array_equal(np.isnan(g), np.isnan(v)), f"NaN pattern of d{k}"
+        assert rel_err(g, v) <= gtol, (k, rel_err(g, v))
+
+
+def test_default_noise_is_the_reference_cpu_draw():
+    """mpvae_noise unset: noise comes from torch's CPU generator exactly like
+    mpvae.py:162, so seeding reproduces the golden run with no noise handed in."""
+    f = FIX[0]
+    t = _inputs(f, grads=False)
+    torch.manual_seed(1000 + 11)  # the seed make_golden.py used for f1
+    out = _call(t, f.args())
+    for k, o in zip(OUTS, out):
+        assert rel_err(_np(o), f["out_" + k]) <= FWD_RTOL, k
+
+
+def test_philox_kernel_known_answers():
+    lib = H.load_library()
+    out = torch.empty(4 * 3, dtype=torch.int32, device=DEV)
+    H.check(lib.mpv_philox_raw(H.ptr(out), 3, 0, 0, H.stream_of(DEV)), "philox_raw")
+    got = out.cpu().numpy().view(np.uint32).reshape(3, 4)
+    ref = np.stack(philox.philox4x32_10(np.arange(3), 0, 0, 0, 0, 0), -1)
+    np.testing.assert_array_equal(got, ref)
+    H.check(lib.mpv_philox_raw(H.ptr(out), 1, 0xFFFFFFFFFFFFFFFF, 0xFFFFFFFFFFFFFFFF,
+                               H.stream_of(DEV)), "philox_raw")
+    got = tuple(int(x) for x in out[:4].cpu().numpy().view(np.uint32))
+    # counter (0xffffffff, 0xffffffff, 0, 0): compare with the oracle
+    want = tuple(int(x) for x in philox.philox4x32_10(0xffffffff, 0xffffffff, 0, 0,
+                                                      0xffffffff, 0xffffffff))
+    assert got == want
+
+
+@pytest.mark.parametrize("S,B,z,s_off", [(7, 5, 13, 0), (9, 3, 38, 5), (64, 16, 128, 100)])
+def test_philox_noise_matches_oracle(S, B, z, s_off):
+    be = HipShardBackend()
+    shape = H.Shape(S, s_off + S, s_off, B, 4, z)
+    eps = be.make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
+    ref = philox.normal_noise(S, B, z, seed=0x1234ABCD5678, s_offset=s_off)
+    np.testing.assert_allclose(_np(eps), ref, atol=2e-5, rtol=2e-5)
+
+
+RANDOM_CASES = [
+    # L, z, B, S, d   (edge tiles: non-multiples of 4/16/32/128, several K chunks)
+    (38, 38, 128, 100, 50),      # C2 shape at S/10
+    (81, 81, 16, 200, 50),       # C3 label dim
+    (100, 37, 3, 130, 8),        # z % 4 != 0, ragged everything
+    (200, 64, 5, 257, 8),        # two column tiles, ragged s tiles
+    (1024, 1024, 2, 48, 50),     # C4 dims, tiny batch
+    (1030, 96, 2, 20, 8),        # L > 1024: two bwd column chunks
+]
+
+
+@pytest.mark.parametrize("L,z,B,S,d", RANDOM_CASES)
+def test_random_against_oracle(L, z, B, S, d):
+    rng = np.random.default_rng(L * 7 + S)
+    y = (rng.random((B, L)) < 0.25).astype(np.float32)
+    y[:, 0], y[:, 1] = 1, 0
+    f32 = lambda a: a.astype(np.float32)
+    inp = dict(y=y, fe_out=f32(rng.standard_normal((B, L))), fx_out=f32(rng.standard_normal((B, L))),
+               fe_mu=f32(rng.standard_normal((B, d))), fe_logvar=f32(0.3 * rng.standard_normal((B, d))),
+               fx_mu=f32(rng.standard_normal((B, d))), fx_logvar=f32(0.3 * rng.standard_normal((B, d))),
+               r_sqrt_sigma=rng.uniform(-1, 1, (L, z)) * np.sqrt(6.0 / (L + z)))
+    noise = f32(rng.standard_normal((S, B, z)))
+    g_I, g_IL = f32(rng.standard_normal((B, L))), f32(rng.standard_normal((B, L)))
+    ref = pe.elbo_forward(inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"], inp["fx_out"],
+                          inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, 0.5, 10.0)
+    rg = pe.elbo_backward(ref, inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"],
+                          inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, 0.5, 10.0,
+                          g_total=1.0, g_I=g_I, g_IL=g_IL)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in inp.items()}
+    for k in DIFF + ["r_sqrt_sigma"]:
+        t[k].requires_grad_(True)
+    args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
+                              mode="train", nll_coeff=0.5, c_coeff=10.0,
+                              mpvae_noise=torch.from_numpy(noise))
+    out = _call(t, args)
+    for k, o in zip(OUTS, out):
+        assert rel_err(_np(o), ref[k]) <= FWD_RTOL, (k, rel_err(_np(o), ref[k]))
+    obj = out[0] + (out[6] * torch.from_numpy(g_I).to(DEV)).sum() + \
+        (out[7] * torch.from_numpy(g_IL).to(DEV)).sum()
+    obj.backward()
+    for k in DIFF + ["r_sqrt_sigma"]:
+        e = rel_err(_np(t[k].grad), rg[k])
+        assert e <= GRAD_RTOL, (k, e)
+
+
+def test_shard_invariance_at_c4_size():
+    """Size-independent property at the headline size (B=512, S=4096, L=z=1024):
+    two S-shards combined exactly equal one unsharded evaluation (philox noise
+    is keyed on the global sample index)."""
+    B, S, L, z, d = 512, 4096, 1024, 1024, 50
+    g = torch.Generator(device=DEV).manual_seed(3)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    mus = [torch.randn((B, d), device=DEV, generator=g) for _ in range(4)]
+    R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
+         * (6.0 / (L + z)) ** 0.5)
+    be = HipShardBackend()
+    R32 = be.to_f32(R)
+    seed = 987654321
+
+    def local(S_loc, s_off):
+        shape = be.shape(S_loc, S, s_off, B, L, z)
+        eps = be.make_noise(shape, DEV, seed, 0)
+        return shape, be.forward_local(shape, y, fe, fx, R32, eps, keep_T=False)
+
+    shape, full = local(S, 0)
+    out_full = be.finalize(shape, full["bstat"], full["colsum"], *mus, 0.5, 10.0)
+    _, a = local(1536, 0)
+    _, b = local(S - 1536, 1536)
+    bstat = be.combine_bstats(torch.stack([a["bstat"], b["bstat"]]))
+    colsum = a["colsum"] + b["colsum"]
+    out_sh = be.finalize(shape, bstat, colsum, *mus, 0.5, 10.0)
+    for k, o1, o2 in zip(OUTS, out_full, out_sh):
+        assert torch.isfinite(o1).all(), k
+        assert rel_err(_np(o2), _np(o1)) <= 1e-5, k
+    p = _np(out_full[6])
+    assert (p > 0).all() and (p < 1).all()
+
+
+def test_full_size_train_step_is_finite_and_deterministic():
+    """C4 forward+backward with philox noise: finite, and bitwise reproducible
+    (no atomics anywhere in the kernels)."""
+    B, S, L, z, d = 512, 4096, 1024, 1024, 50
+    g = torch.Generator(device=DEV).manual_seed(5)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    base = [torch.randn((B, L), device=DEV, generator=g) for _ in range(2)]
+    mus = [torch.randn((B, d), device=DEV, generator=g) for _ in range(4)]
+    R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.03)
+    args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
+                              mode="train", nll_coeff=0.1, c_coeff=200.0, mpvae_noise="philox",
+                              mpvae_seed=42)
+    res = []
+    for _ in range(2):
+        leaves = [x.clone().requires_grad_(True) for x in [base[0], mus[0], mus[1], base[1],
+                                                            mus[2], mus[3], R]]
+        out = mpvae.compute_loss(y, *leaves, args)
+        out[0].backward()
+        res.append([out[0].detach().clone()] + [x.grad.clone() for x in leaves])
+    for a, b in zip(*res):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+
+
+def test_test_mode_forward_only_large_s():
+    f = next(f for f in FIX if f.name == "f5_testmode")
+    t = _inputs(f, grads=False)
+    args = f.args(n_test_sample=10000, mpvae_noise="philox", mpvae_seed=1)
+    with torch.no_grad():
+        out = _call(t, args)
+    assert all(torch.isfinite(o).all() for o in out)
+    # 10000-sample MC estimate of indiv_prob vs the fixture's 24-sample estimate
+    assert np.abs(_np(out[6]) - f["out_indiv_prob"]).max() < 0.25
+
+
+def test_inplace_total_and_partial_outputs():
+    """Callers do `total_loss += fairloss` and backprop only through
+    indiv_prob (fairsoft_train.py:137, fairsoft_train_postprocess.py:121-167)."""
+    f = FIX[0]
+    t = _inputs(f)
+    out = _call(t, f.args(mpvae_noise=torch.from_numpy(f["noise"])))
+    total = out[0]
+    total += (out[6] ** 2).sum()
+    total.backward()
+    assert torch.isfinite(t["fe_out"].grad).all()
+    t2 = _inputs(f)
+    out2 = _call(t2, f.args(mpvae_noise=torch.from_numpy(f["noise"])))
+    out2[6].sum().backward()
+    ref = pe.elbo_forward(f["y"], f["fe_out"], f["fe_mu"], f["fe_logvar"], f["fx_out"],
+                          f["fx_mu"], f["fx_logvar"], f["r_sqrt_sigma"], f["noise"],
+                          f.nll_coeff, f.c_coeff)
+    rg = pe.elbo_backward(ref, f["y"], f["fe_out"], f["fe_mu"], f["fe_logvar"], f["fx_out"],
+                          f["fx_mu"], f["fx_logvar"], f["noise"], f.nll_coeff, f.c_coeff,
+                          g_I=np.ones_like(f["g_I"]))
+    assert rel_err(_np(t2["fx_out"].grad), rg["fx_out"]) <= GRAD_RTOL
+    assert float(t2["fe_out"].grad.abs().max()) == 0.0
+    assert t2["fe_mu"].grad is None or float(t2["fe_mu"].grad.abs().max()) == 0.0

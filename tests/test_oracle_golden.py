@@ -1,0 +1,102 @@
+"""Pin the CPU oracle against the reference's own outputs (golden vectors made
+by importing /root/reference/mpvae.py, tests/golden/make_golden.py) and the
+Philox oracle against the published Random123 known-answer vectors."""
+import numpy as np
+import pytest
+
+from golden_io import OUTS, PART_KEYS, fixtures
+from oracle import philox, probit_elbo as pe
+from tolerances import (EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL, rel_err)
+
+FIX = fixtures()
+
+
+def _fwd(f, ranking, shards):
+    return pe.elbo_forward(f["y"], f["fe_out"], f["fe_mu"], f["fe_logvar"], f["fx_out"],
+                           f["fx_mu"], f["fx_logvar"], f["r_sqrt_sigma"], f["noise"],
+                           f.nll_coeff, f.c_coeff, ranking=ranking, shards=shards)
+
+
+@pytest.mark.parametrize("f", FIX, ids=[f.name for f in FIX])
+@pytest.mark.parametrize("ranking", ["naive", "factorized"])
+@pytest.mark.parametrize("shards", [1, 3])
+def test_oracle_forward_matches_reference(f, ranking, shards):
+    if shards > f.S:
+        pytest.skip("fewer samples than shards")
+    out = _fwd(f, ranking, shards)
+    tol = EXTREME_FWD_RTOL if f.extreme else FWD_RTOL
+    for k in OUTS:
+        assert rel_err(out[k], f["out_" + k]) <= tol, (k, rel_err(out[k], f["out_" + k]))
+
+
+@pytest.mark.parametrize("f", [f for f in FIX if f.mode == "train"],
+                         ids=[f.name for f in FIX if f.mode == "train"])
+@pytest.mark.parametrize("kind", ["gtot", "gpart"])
+def test_oracle_backward_matches_reference(f, kind):
+    out = _fwd(f, "factorized", 2 if f.S >= 2 else 1)
+    if kind == "gtot":
+        up = dict(g_total=1.0, g_I=f["g_I"], g_IL=f["g_IL"])
+    else:
+        up = dict(zip(PART_KEYS, f["a_parts"]))
+    g = pe.elbo_backward(out, f["y"], f["fe_out"], f["fe_mu"], f["fe_logvar"], f["fx_out"],
+                         f["fx_mu"], f["fx_logvar"], f["noise"], f.nll_coeff, f.c_coeff, **up)
+    ref = f.grads(kind)
+    assert ref, "fixture has no gradients"
+    tol = EXTREME_GRAD_RTOL if f.extreme else GRAD_RTOL
+    for k, v in ref.items():
+        assert np.array_equal(np.isnan(g[k]), np.isnan(v)), f"NaN pattern of d{k}"
+        assert rel_err(g[k], v) <= tol, (k, rel_err(g[k], v))
+
+
+def test_degenerate_rows_nan_pattern():
+    """All-0 / all-1 label rows: ranking loss 0 forward, whole-row NaN gradient
+    (mpvae.py:117-121 under autograd) -- pinned by fixture f2."""
+    f = next(f for f in FIX if f.name == "f2_degenerate")
+    g = f.grads("gtot")
+    rows = np.isnan(g["fe_out"]).all(1)
+    assert rows.tolist() == [False, True, False, False, True, False, False, False]
+    assert np.isnan(g["r_sqrt_sigma"]).all()
+    assert not np.isnan(g["fe_mu"]).any()
+
+
+def test_philox_known_answers():
+    """Random123 kat_vectors for philox4x32_10."""
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = philox.philox4x32_10(*ctr, *key)
+        assert tuple(int(x) for x in got) == want
+
+
+def test_philox_noise_is_standard_normal_and_shard_invariant():
+    n = philox.normal_noise(64, 16, 24, seed=77)
+    assert abs(n.mean()) < 0.01 and abs(n.std() - 1.0) < 0.01
+    a = philox.normal_noise(40, 16, 24, seed=77, s_offset=24)
+    np.testing.assert_array_equal(a, n[24:64])
+
+
+@pytest.mark.parametrize("f", [f for f in FIX if f.mode == "train"][:4],
+                         ids=[f.name for f in FIX if f.mode == "train"][:4])
+def test_torch_restatement_matches_reference(f):
+    """oracle.torch_ref (the bench CPU baseline) reproduces the golden outputs
+    and gradients: it is the reference algorithm, op for op."""
+    import torch
+    from oracle import torch_ref
+    from golden_io import DIFF
+    t = {k: torch.from_numpy(f[k].copy()) for k in ["y", "fe_out", "fe_mu", "fe_logvar",
+                                                     "fx_out", "fx_mu", "fx_logvar",
+                                                     "r_sqrt_sigma", "noise"]}
+    for k in DIFF:
+        t[k].requires_grad_(True)
+    out = torch_ref.elbo_naive(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
+                               t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], t["noise"],
+                               f.nll_coeff, f.c_coeff)
+    for k, o in zip(OUTS, out):
+        assert rel_err(o.detach().numpy(), f["out_" + k]) <= 1e-6, k
+    obj = out[0] + (out[6] * torch.from_numpy(f["g_I"])).sum() + \
+        (out[7] * torch.from_numpy(f["g_IL"])).sum()
+    obj.backward()
+    for k in DIFF:
+        assert rel_err(t[k].grad.numpy(), f["gtot_" + k]) <= 1e-5, k

@@ -1,0 +1,38 @@
+"""Stated tolerances of the parity tests (fp32 arithmetic, like the reference).
+
+Error metric: normwise relative error  max|a - b| / max|b|  over one output
+tensor (NaN positions must match exactly and are excluded from the metric).
+
+Why these numbers: the reference itself is fp32; against our fp64-reduction
+oracle it differs by <= 2.4e-7 (forward) and <= 4.8e-6 (gradients) on the
+non-extreme fixtures (measured, tests/test_oracle_golden.py).  A second fp32
+implementation (the GPU kernels: different erf/log/exp ulps, different
+summation order, MFMA fma chains) is allowed the same order of error with
+headroom.  The extreme-logit fixture (|u| up to ~20) is different in kind:
+E = Phi(u)(1-1e-6)+0.5e-6 evaluates 1 + erf(x) in fp32 near erf = -1, where
+one ulp of erf is a few percent of E; the reference's own torch-CPU erf and
+scipy's erf disagree there by up to 1.3e-2 in the gradient.  That fixture is
+checked at the looser level.
+"""
+
+FWD_RTOL = 2e-5
+GRAD_RTOL = 5e-5
+EXTREME_FWD_RTOL = 1e-3
+EXTREME_GRAD_RTOL = 5e-2
+
+
+def rel_err(a, b):
+    import numpy as np
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return float("inf")
+    m = ~nb
+    if not m.any():
+        return 0.0
+    scale = np.max(np.abs(b[m]))
+    err = np.max(np.abs(a[m] - b[m]))
+    if scale == 0.0:
+        return float(err)
+    return float(err / scale)
