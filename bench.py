@@ -112,6 +112,21 @@ def roofline(times, S_local, B, L, z, steps):
             "per_launch_ms": breakdown}
 
 
+def pmc_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary for this config (profiles/r*_<config>_pmc.json, tools/profile.sh +
+    tools/pmc_summary.py); None when no profile of this kernel exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    k = data.get("kernels", {}).get(kernel)
+    if not k or k.get("hbm_bytes_per_launch") is None:
+        return None, None
+    return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(L, z, B, d, S_cpu, reps, device):
     """Reference algorithm restated in torch (oracle/torch_ref.py) on the host
     cores, fwd+bwd on a bounded slice of the workload; also the ELBO rel-err of
@@ -202,6 +217,7 @@ def main():
     finite = bool(torch.isfinite(out[0]).item())
     value = S_total * B * L * cli.steps / elapsed
     rl = roofline(times, S_local, B, L, z, cli.steps)
+    rl["traffic"], rl["traffic_source"] = pmc_traffic(cli.config, rl["kernel"])
 
     cpu, errs = None, None
     if rank == 0 and world == 1 and not cli.no_cpu_baseline:

@@ -1,0 +1,80 @@
+"""Multi-rank S-sharding on CPU (gloo, world_size 2 and 3): the product's
+autograd Function + cross-rank exchange (mpvae_dist) with an oracle shard
+backend must reproduce the unsharded golden values and gradients."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mpvae_dist import SampleShardExchange, split_samples
+from mpvae_ops import ElboConfig, ProbitELBO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, names, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golden_io import DIFF, OUTS, fixtures
+        from oracle_backend import OracleShardBackend
+        from tolerances import FWD_RTOL, GRAD_RTOL, rel_err
+        res = []
+        for f in [f for f in fixtures() if f.name in names]:
+            S_local, s_off = split_samples(f.S, world, rank)
+            t = {k: torch.from_numpy(f[k].copy()) for k in
+                 ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar",
+                  "r_sqrt_sigma"]}
+            for k in DIFF + (["r_sqrt_sigma"] if f.trainable_r else []):
+                t[k].requires_grad_(True)
+            noise = torch.from_numpy(f["noise"][s_off:s_off + S_local].copy())
+            cfg = ElboConfig(f.S, S_local, s_off, f.nll_coeff, f.c_coeff,
+                             backend=OracleShardBackend(), exchange=SampleShardExchange())
+            out = ProbitELBO.apply(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
+                                   t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], noise, cfg)
+            errs = {k: rel_err(o.detach().numpy(), f["out_" + k]) for k, o in zip(OUTS, out)}
+            obj = out[0] + (out[6] * torch.from_numpy(f["g_I"])).sum() + \
+                (out[7] * torch.from_numpy(f["g_IL"])).sum()
+            obj.backward()
+            for k, v in f.grads("gtot").items():
+                errs["d" + k] = rel_err(t[k].grad.numpy(), v)
+            ok = all(v <= (FWD_RTOL if not k.startswith("d") else GRAD_RTOL)
+                     for k, v in errs.items())
+            res.append((f.name, ok, errs))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_elbo_matches_unsharded_reference(world):
+    names = ["f1_l38", "f2_degenerate", "f3_adult_like"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, names, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in results:
+        assert len(res) == len(names)
+        for name, ok, errs in res:
+            assert ok, (rank, name, errs)
+
+
+def test_split_samples_covers_axis():
+    for n, w in [(10, 3), (4096, 8), (7, 7), (1000, 6)]:
+        parts = [split_samples(n, w, r) for r in range(w)]
+        assert sum(p[0] for p in parts) == n
+        assert [p[1] for p in parts] == list(np.cumsum([0] + [p[0] for p in parts])[:-1])

@@ -1,0 +1,114 @@
+"""GPU: the VAE module (fused two-encoder reparameterisation kernel) and the
+drop-in training step, against the reference's golden eval outputs and a
+reference-order torch restatement (oracle/torch_ref.py) on the same device."""
+import argparse
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mpvae
+from golden_io import GOLDEN
+from oracle import torch_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _args(**kw):
+    a = argparse.Namespace(feature_dim=20, latent_dim=8, label_dim=6, z_dim=4, keep_prob=0.5,
+                           scale_coeff=1.0, residue_sigma="", n_train_sample=16,
+                           n_test_sample=16, mode="train", nll_coeff=0.5, c_coeff=10.0)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def _seeded_model(args, seed=0):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    return mpvae.VAE(args)
+
+
+def test_eval_forward_matches_reference_golden():
+    z = np.load(os.path.join(GOLDEN, "vae_small.npz"))
+    model = _seeded_model(_args()).to(DEV).eval()
+    eps = iter([torch.from_numpy(z["eps_label"]).to(DEV), torch.from_numpy(z["eps_feat"]).to(DEV)])
+    model.reparam_noise = lambda like: next(eps)
+    with torch.no_grad():
+        out = model(torch.from_numpy(z["label"]).to(DEV), torch.from_numpy(z["feat"]).to(DEV))
+    names = ["label_out", "label_mu", "label_logvar", "feat_out", "feat_mu", "feat_logvar"]
+    for n, o in zip(names, out):
+        np.testing.assert_allclose(o.cpu().numpy(), z["eval_" + n], rtol=1e-4, atol=1e-5,
+                                   err_msg=n)
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_forward_and_grads_match_reference_order(train):
+    """Same cuda seed -> same dropout masks and eps as the reference's forward
+    order; outputs and all parameter gradients agree with torch autograd."""
+    args = _args()
+    model = _seeded_model(args).to(DEV).train(train)
+    label = (torch.rand(7, 6, device=DEV) < 0.4).float()
+    feat = torch.randn(7, 20, device=DEV)
+    torch.cuda.manual_seed(123)
+    ours = model(label, feat)
+    w = [torch.randn_like(o) for o in ours]
+    sum((o * wi).sum() for o, wi in zip(ours, w)).backward()
+    g_ours = {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad()
+    torch.cuda.manual_seed(123)
+    ref = torch_ref.vae_forward_reference_order(model, label, feat)
+    sum((o * wi).sum() for o, wi in zip(ref, w)).backward()
+    for a, b in zip(ours, ref):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            assert k not in g_ours
+            continue
+        torch.testing.assert_close(g_ours[k], p.grad, rtol=1e-4, atol=1e-6, msg=k)
+
+
+def _has_finite_grad(model):  # fairsoft_utils.py:28-41
+    return all(torch.isfinite(p.grad).all() for p in model.parameters() if p.grad is not None)
+
+
+def _train_steps(use_ours, steps=3):
+    """The live loop body of fairsoft_train.py:45-146 (penalty-free): forward ->
+    compute_loss -> backward -> clip 10 -> finite gate -> Adam step."""
+    args = _args(feature_dim=30, label_dim=12, z_dim=12, latent_dim=8, n_train_sample=32)
+    model = _seeded_model(args, seed=7).to(DEV).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(3 * 16, 30, generator=g)
+    Y = (torch.rand(3 * 16, 12, generator=g) < 0.3).float()
+    Y[:, 0], Y[:, 1] = 1, 0
+    torch.manual_seed(5)
+    torch.cuda.manual_seed(5)
+    losses = []
+    for i in range(steps):
+        opt.zero_grad()
+        feat, label = X[16 * i:16 * (i + 1)].to(DEV), Y[16 * i:16 * (i + 1)].to(DEV)
+        if use_ours:
+            out = model(label, feat)
+            res = mpvae.compute_loss(label, *out, model.r_sqrt_sigma, args)
+        else:
+            out = torch_ref.vae_forward_reference_order(model, label, feat)
+            noise = torch.normal(0, 1, size=(32, 16, 12)).to(DEV)   # mpvae.py:162
+            res = torch_ref.elbo_naive(label, *out, model.r_sqrt_sigma, noise, args.nll_coeff,
+                                       args.c_coeff)
+        res[0].backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 10.0)
+        if _has_finite_grad(model):
+            opt.step()
+        losses.append(float(res[0].detach()))
+    return losses, {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+
+def test_dropin_training_loop_tracks_reference():
+    l1, p1 = _train_steps(True)
+    l2, p2 = _train_steps(False)
+    np.testing.assert_allclose(l1, l2, rtol=1e-4)
+    for k in p1:
+        torch.testing.assert_close(p1[k], p2[k], rtol=1e-3, atol=1e-5, msg=k)

@@ -1,0 +1,63 @@
+"""VAE drop-in on CPU (construction only -- no kernel runs): same parameter
+names, order, shapes, dtypes and seeded init as the reference (golden
+fingerprints from tests/golden/make_golden.py), checkpoint round trip."""
+import argparse
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mpvae
+from golden_io import GOLDEN
+
+
+def _args(residue_sigma=""):
+    return argparse.Namespace(feature_dim=20, latent_dim=8, label_dim=6, z_dim=4, keep_prob=0.5,
+                              scale_coeff=1.0, residue_sigma=residue_sigma)
+
+
+@pytest.fixture(scope="module")
+def gold():
+    z = np.load(os.path.join(GOLDEN, "vae_small.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def test_state_dict_layout_and_seeded_init(gold):
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = mpvae.VAE(_args())
+    sd = model.state_dict()
+    assert list(sd.keys()) == list(gold["sd_names"])
+    assert len(sd) == 31
+    for i, (k, v) in enumerate(sd.items()):
+        shp = [s for s in gold["sd_shapes"][i] if s] or []
+        assert list(v.shape) == shp[:v.dim()] or list(v.shape) == shp, k
+        assert str(v.dtype) == gold["sd_dtypes"][i], k
+        np.testing.assert_allclose(v.double().sum().item(), gold["sd_sums"][i], rtol=1e-9,
+                                   atol=1e-9, err_msg=k)
+        np.testing.assert_allclose(v.reshape(-1)[:4].double().numpy(), gold["sd_head"][i],
+                                   rtol=0, atol=0, err_msg=k)
+
+
+def test_shared_decoder_and_r_sqrt_sigma_modes():
+    m = mpvae.VAE(_args())
+    assert m.fd1 is m.fd_x1 and m.fd2 is m.fd_x2
+    assert m.r_sqrt_sigma.dtype == torch.float64 and m.r_sqrt_sigma.requires_grad
+    r = mpvae.VAE(_args("random")).r_sqrt_sigma
+    assert r.dtype == torch.float64 and not r.requires_grad
+    zr = mpvae.VAE(_args("zero")).r_sqrt_sigma
+    assert zr.dtype == torch.float32 and not zr.requires_grad and float(zr.abs().sum()) == 0.0
+    assert m.dropout.p == 0.5
+
+
+def test_checkpoint_round_trip(tmp_path):
+    torch.manual_seed(1)
+    np.random.seed(1)
+    a = mpvae.VAE(_args())
+    p = tmp_path / "vae.pkl"
+    torch.save(a.state_dict(), p)
+    b = mpvae.VAE(_args())
+    b.load_state_dict(torch.load(p, weights_only=True))
+    for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert ka == kb and torch.equal(va, vb)

@@ -1,0 +1,65 @@
+"""Summarise a tools/profile.sh run into profiles/<round>_<tag>_*.
+
+  kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
+  pmc.json           per kernel: launches, avg duration (trace), avg FETCH_SIZE /
+                     WRITE_SIZE (KiB, as reported) and corrected HBM bytes per launch
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
+the bytes of a wide (16 B/lane) coalesced read -> x2; WRITE_SIZE is exact for
+16 B/lane stores.  Both counters are KiB.  All loads/stores of the kernels
+summarised here are 16 B/lane (float4) except where noted in DESIGN.md.
+
+usage: python tools/pmc_summary.py gpurun_out/prof/c4 profiles r01_c4
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def short(name):
+    name = name.split("(")[0]
+    for pre in ("void ", "mpv::"):
+        name = name.replace(pre, "")
+    return name.split("<")[0].replace("_kernel", "")
+
+
+def counters(path, counter):
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        agg.setdefault(short(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(src, dst, tag):
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "trace_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    dur = {}
+    for r in csv.DictReader(open(stats)):
+        k = short(r["Name"])
+        if not r["Name"].startswith(("void mpv::", "mpv::")):
+            continue
+        dur[k] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6)
+    fetch = counters(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write = counters(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
+    out = {"source": src, "note": "bytes per launch; fetch corrected x2 (gfx950 FETCH_SIZE "
+                                  "reports half of 16B/lane reads)", "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f_kib, w_kib = fetch.get(k), write.get(k)
+        hbm = None
+        if f_kib is not None and w_kib is not None:
+            hbm = (2.0 * f_kib + w_kib) * 1024.0
+        out["kernels"][k] = {"launches_traced": dur.get(k, (None,))[0],
+                             "avg_ms_trace": dur.get(k, (None, None))[1],
+                             "fetch_size_kib": f_kib, "write_size_kib": w_kib,
+                             "hbm_bytes_per_launch": hbm}
+    json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])

@@ -1,0 +1,30 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench workload (run on the GPU box via gpurun):
+#   1. kernel trace + stats (per-kernel durations)
+#   2. PMC FETCH_SIZE pass, 3. PMC WRITE_SIZE pass (separate passes: TCC slots)
+# Outputs under gpurun_out/prof/<tag>/; copy the summaries into profiles/.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${TAG:-c4}"
+ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}"
+OUT="$R/gpurun_out/prof/$TAG"
+KRE="${KRE:-probit_fwd|dR_gemm|bwd_elem|noise_philox}"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" -f csv -d "$OUT/$name" -o "$name" -- \
+      python3 "$R/bench.py" $ARGS > "$OUT/$name.json" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "[$name] rc=$rc"
+  [ $rc -eq 0 ] || { tail -20 "$OUT/$name.err"; exit $rc; }
+}
+STEPS="${STEPS:-trace fetch write}"
+for s in $STEPS; do
+  case $s in
+    trace) run trace --kernel-trace --stats ;;
+    fetch) run fetch --pmc FETCH_SIZE --kernel-include-regex "$KRE" ;;
+    write) run write --pmc WRITE_SIZE --kernel-include-regex "$KRE" ;;
+  esac
+done
+find "$OUT" -name "*.csv" | head -20
