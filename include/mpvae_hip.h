@@ -64,6 +64,33 @@ int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t
  * philox(counter = ctr0 + i (as lo,hi,0,0), key = key). */
 int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* stream);
 
+/* 3xf16 split operand of the noise GEMMs: value = (hi + lo) / *scale, with hi
+ * and lo fp16 planes of shape (rows_pad, ld), zero padded, and *scale a power
+ * of two chosen on the device from max|x| (mpv_split_f16) or fixed
+ * (mpv_noise_philox_f16).  hi*hi + hi*lo + lo*hi on the f16 matrix cores with
+ * fp32 accumulation reproduces an fp32 product to ~2^-22. */
+typedef struct mpv_split16 {
+  uint16_t* hi;
+  uint16_t* lo;
+  float* scale;      /* device scalar */
+  int64_t rows_pad;  /* allocated rows */
+  int64_t ld;        /* row length in elements, multiple of 8 */
+} mpv_split16;
+
+enum mpv_gemm { MPV_GEMM_F16X3 = 0, MPV_GEMM_F32 = 1 };
+
+size_t mpv_split_workspace_bytes(void);
+
+/* x (rows, cols) fp32 / fp64 -> split planes.  Used for r_sqrt_sigma
+ * (replacing R.T.float(), mpvae.py:165) and for explicit noise. */
+int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const mpv_split16* out,
+                  void* workspace, void* stream);
+
+/* mpv_noise_philox writing split planes directly (rows = S_local*B, row = s*B+b);
+ * the same numbers as mpv_noise_philox. */
+int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                         const mpv_split16* out, void* stream);
+
 /* Element-wise dtype conversion; replaces r_sqrt_sigma.T.float() (mpvae.py:165)
  * and the fp32 -> fp64 cast of its gradient in autograd. */
 int mpv_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
@@ -74,8 +101,11 @@ typedef struct mpv_fwd_args {
   const float* y;
   const float* fe_out;
   const float* fx_out;
-  const float* R32;     /* (L,z) fp32 */
-  const float* eps;     /* (S_local,B,z) */
+  int gemm;             /* mpv_gemm: which operand pair below is used */
+  const float* R32;     /* MPV_GEMM_F32:   (L,z) fp32 */
+  const float* eps;     /*                 (S_local,B,z) fp32 */
+  mpv_split16 R16;      /* MPV_GEMM_F16X3: R planes, rows_pad >= roundup(L,128), ld >= roundup(z,128) */
+  mpv_split16 eps16;    /*                 noise planes, rows = S_local*B, ld as R16.ld */
   float* T;             /* (B,S_local,L) or NULL when no backward will follow */
   float* rowstat;       /* (6,B,S_local) out */
   float* bstat;         /* (6,B) out: this shard's statistics */
@@ -127,8 +157,12 @@ typedef struct mpv_bwd_args {
   const float* y;
   const float* fe_out;
   const float* fx_out;
-  const float* eps;            /* (S_local,B,z), the forward's noise */
-  float* T;                    /* in: forward's T; clobbered with d(sample_r)+d(sample_r_x) */
+  int gemm;                    /* mpv_gemm, as in the forward */
+  const float* eps;            /* MPV_GEMM_F32: (S_local,B,z), the forward's noise */
+  mpv_split16 eps16;           /* MPV_GEMM_F16X3: the forward's noise planes */
+  float* T;                    /* in: forward's T; MPV_GEMM_F32 overwrites it with
+                                  d(sample_r)+d(sample_r_x) (F16X3 writes planes in
+                                  the workspace instead) */
   const float* rowstat;        /* (6,B,S_local) from the forward */
   const float* bstat;          /* (6,B) GLOBAL statistics */
   const float* gscal;          /* (6) device: upstream grads, mpv_gslot order */
@@ -142,7 +176,7 @@ typedef struct mpv_bwd_args {
   size_t workspace_bytes;
 } mpv_bwd_args;
 
-size_t mpv_bwd_workspace_bytes(const mpv_shape* shape);
+size_t mpv_bwd_workspace_bytes(const mpv_shape* shape, int gemm);
 
 /* Replaces PyTorch autograd through mpvae.py:165-210 (including the pairwise
  * (S,B,L,L) ranking tensor): d fe_out, d fx_out and d r_sqrt_sigma. */

@@ -71,6 +71,34 @@ MPV_DEV float block_reduce(float v, float* red) {
   return r;
 }
 
+// ---- 3xf16 split operands ---------------------------------------------------
+// x*s = hi + lo with hi = fp16(x*s), lo = fp16(x*s - hi); the power-of-two
+// scale s keeps max|x*s| <= 2^15 so both halves stay in the fp16 normal range
+// for every element that matters.  A product is evaluated as
+// hi*hi + hi*lo + lo*hi on the f16 matrix cores with fp32 accumulation
+// (the dropped lo*lo term is <= 2^-22 relative).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+MPV_DEV void split_f16(float x, float s, uint16_t& hi, uint16_t& lo) {
+  const float xs = x * s;
+  const _Float16 h = (_Float16)xs;
+  const _Float16 l = (_Float16)(xs - (float)h);
+  hi = __builtin_bit_cast(uint16_t, h);
+  lo = __builtin_bit_cast(uint16_t, l);
+}
+
+// Power-of-two scale mapping max|x| to (2^13, 2^14]; 1 for 0 / non-finite.
+MPV_DEV float pow2_scale(float maxabs) {
+  if (!(maxabs > 0.0f) || !isfinite(maxabs)) return 1.0f;
+  int e;
+  frexpf(maxabs, &e);           // maxabs = m * 2^e, m in [0.5, 1)
+  return ldexpf(1.0f, 14 - e);  // maxabs * s in [2^13, 2^14)
+}
+
+MPV_DEV f16x8 as_f16x8(s16x8 v) { return __builtin_bit_cast(f16x8, v); }
+
 // ---- Philox4x32-10 (Salmon et al. SC'11) ------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 

@@ -4,15 +4,19 @@
 //   bwd_coef_kernel  per (s,b): alpha = -g_nll * softmax_s(logp)/B and the
 //                    ranking coefficients betaP = g_c N/(n S B), betaN = g_c P/(n S B)
 //                    (NaN for a degenerate row whose ranking term is live,
-//                    reproducing the 0/0 of mpvae.py:118 under autograd)
+//                    reproducing the 0/0 of mpvae.py:118 under autograd); per
+//                    batch row also an upper bound of |G| (3xf16 scale).
 //   bwd_elem_kernel  streams T once: recomputes E, E_x, forms
 //                    dE = alpha (y/E - (1-y)/(1-E)) - [y=1] betaP e^{-5E}
 //                         + [y=0] betaN e^{5E} + g_indiv/S,
 //                    du = dE (1-1e-6) phi(u); column sums over s give d fe_out /
-//                    d fx_out; writes G = du + du_x over T.
-//   dR_gemm_kernel   dR[l][k] = sum_{s,b} G[s,b,l] eps[s,b,k] on the fp32
-//                    matrix cores, split-K over the S*B rows into slabs,
-//                    reduced in a fixed order (deterministic).
+//                    d fx_out; writes G = du + du_x (fp32 over T, or 3xf16 planes).
+//   dR16_kernel      dR[l][k] = sum_{s,b} G[s,b,l] eps[s,b,k], 3xf16 operands on
+//                    the f16 matrix cores; the rows (the K axis) are the LDS
+//                    rows, fragments come from ds_read_b64_tr_b16 transposed
+//                    reads; split-K over the S*B rows into slabs reduced in a
+//                    fixed order (deterministic).
+//   dR_gemm_kernel   the same on exact fp32 MFMA (MPV_GEMM_F32).
 #include "abi_util.h"
 #include "mpv_common.h"
 
@@ -20,25 +24,34 @@ namespace mpv {
 
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
                      hipStream_t s);
+int launch_scale(const float* block_max, int n, float* scale, hipStream_t s);
+
+// Upper bounds used for the G scale (3xf16): for E = Phi(u)(1-1e-6)+0.5e-6,
+// sup_u phi(u) |y/E - (1-y)/(1-E)| < 4.5 (inverse Mills ratio capped by the
+// 0.5e-6 floor), phi(u) e^{-5E} <= 0.4, phi(u) e^{5E} <= 0.4 e^5 < 60.  Only the
+// order of magnitude matters: the split keeps full precision for anything
+// within 2^10 of the bound.
+constexpr float kBoundDl = 4.5f, kBoundPos = 0.4f, kBoundNeg = 60.0f, kBoundInd = 0.4f;
 
 // --------------------------------------------------------------- coefficients
-__global__ __launch_bounds__(256) void bwd_coef_kernel(const float* __restrict__ y,
-                                                      const float* __restrict__ rowstat,
-                                                      const float* __restrict__ bstat,
-                                                      const float* __restrict__ gscal,
-                                                      float* __restrict__ coef, int S, int B,
-                                                      int L, float S_total, float nll_coeff,
-                                                      float c_coeff, int live) {
+__global__ __launch_bounds__(256) void bwd_coef_kernel(
+    const float* __restrict__ y, const float* __restrict__ rowstat, const float* __restrict__ bstat,
+    const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
+    float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
+    float nll_coeff, float c_coeff, int live) {
   __shared__ float red[16];
   const int b = blockIdx.x, tid = threadIdx.x;
-  float np = 0.f, nn = 0.f;
+  float np = 0.f, nn = 0.f, gi = 0.f;
   for (int l = tid; l < L; l += blockDim.x) {
-    const float v = y[(int64_t)b * L + l];
+    const int64_t o = (int64_t)b * L + l;
+    const float v = y[o];
     np += (v == 1.0f) ? 1.0f : 0.0f;
     nn += (v == 0.0f) ? 1.0f : 0.0f;
+    gi = fmaxf(gi, (gI ? fabsf(gI[o]) : 0.0f) + (gIL ? fabsf(gIL[o]) : 0.0f));
   }
   np = block_reduce<false>(np, red);
   nn = block_reduce<false>(nn, red);
+  gi = block_reduce<true>(gi, red);
   const float nrm = np * nn;
   const float gt = gscal[MPV_G_TOTAL];
   const float gn[2] = {gscal[MPV_G_NLL] + nll_coeff * gt, gscal[MPV_G_NLL_X] + nll_coeff * gt};
@@ -46,11 +59,13 @@ __global__ __launch_bounds__(256) void bwd_coef_kernel(const float* __restrict__
   const bool clive[2] = {(live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C))) != 0,
                          (live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C_X))) != 0};
   const float inv_B = 1.0f / (float)B;
+  float bound = kBoundInd * gi / S_total;
 #pragma unroll
   for (int br = 0; br < 2; ++br) {
     const float M = bstat[(2 * br) * B + b], Z = bstat[(2 * br + 1) * B + b];
     const bool dead = !(nrm > 0.0f) && clive[br];
     const float cs = gc[br] / (nrm * S_total * (float)B);
+    float bmax = 0.0f;
     for (int s = tid; s < S; s += blockDim.x) {
       const float lp = rowstat[((int64_t)br * B + b) * S + s];
       const float P = rowstat[((int64_t)(2 + 2 * br) * B + b) * S + s];
@@ -58,12 +73,15 @@ __global__ __launch_bounds__(256) void bwd_coef_kernel(const float* __restrict__
       float alpha = -gn[br] * (expf(lp - M) / Z) * inv_B;
       float bP = nrm > 0.0f ? cs * N : 0.0f;
       float bN = nrm > 0.0f ? cs * P : 0.0f;
+      bmax = fmaxf(bmax, kBoundDl * fabsf(alpha) + kBoundPos * fabsf(bP) + kBoundNeg * fabsf(bN));
       if (dead) alpha = bP = bN = __builtin_nanf("");
       coef[((int64_t)(3 * br + 0) * B + b) * S + s] = alpha;
       coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP;
       coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN;
     }
+    bound += block_reduce<true>(bmax, red);
   }
+  if (tid == 0 && gbound) gbound[b] = bound;
 }
 
 // ------------------------------------------------------------ element pass
@@ -75,8 +93,12 @@ struct ElemParams {
   const float* gIL;  // (B,L) grad of indiv_prob_label (label branch) or NULL
   const float* coef;
   float* T;
+  uint16_t* g_hi;    // 3xf16 output planes (B*S rows, ldg), or NULL: fp32 G over T
+  uint16_t* g_lo;
+  const float* g_scale;
+  int64_t ldg;
   float* colpart;  // [nSc][2][B][L]
-  int S, B, L;
+  int S, B, L, Lc;  // Lc: columns covered (L, or ldg for planes: pads get zeros)
   int TPR, RPI, rows_per_chunk;
   float inv_S;
 };
@@ -96,7 +118,7 @@ MPV_DEV float d_elem(float t, float base, float y, bool soft, float alpha, float
   return dE * kC1 * kInvSqrt2Pi * expf(-0.5f * u * u);
 }
 
-template <bool VEC>
+template <bool VEC, bool PLANES>
 __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   __shared__ float cred[256 * 8];
   const int b = blockIdx.x, sc = blockIdx.y;
@@ -105,6 +127,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   const bool active = rsub < p.RPI;
   const int c0 = blockIdx.z * 1024 + cq * 4;
   const int S = p.S, B = p.B, L = p.L;
+  const float gs = PLANES ? *p.g_scale : 1.0f;
 
   float yv[4], fe[4], fx[4], gi[4], gil[4];
   bool ok[4], soft[4];
@@ -123,7 +146,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   float se[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
-  if (active && c0 < L) {
+  if (active && c0 < p.Lc) {
     for (int s = s_begin + rsub; s < s_end; s += p.RPI) {
       const int64_t cb = (int64_t)b * S + s;
       const int64_t BS = (int64_t)B * S;
@@ -143,11 +166,18 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
       for (int q = 0; q < 4; ++q) {
         const float ge = d_elem(t[q], fe[q], yv[q], soft[q], ae, pe, ne, gil[q]);
         const float gx = d_elem(t[q], fx[q], yv[q], soft[q], ax, px, nx, gi[q]);
-        se[q] += ge;
-        sx[q] += gx;
-        G[q] = ge + gx;
+        se[q] += ok[q] ? ge : 0.0f;
+        sx[q] += ok[q] ? gx : 0.0f;
+        G[q] = ok[q] ? ge + gx : 0.0f;
       }
-      if (VEC && c0 + 3 < L) {
+      if (PLANES) {
+        uint16_t h[4], l[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
+        const int64_t o = cb * p.ldg + c0;  // ldg % 4 == 0 and c0 + 3 < ldg
+        *reinterpret_cast<s16x4*>(p.g_hi + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+        *reinterpret_cast<s16x4*>(p.g_lo + o) = s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+      } else if (VEC && c0 + 3 < L) {
         *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
       } else {
 #pragma unroll
@@ -176,6 +206,182 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
       p.colpart[(((int64_t)sc * 2 + 1) * B + b) * L + c] = x;
     }
   }
+}
+
+// ------------------------------------------------------------ 3xf16 dR GEMM
+// LDS image per stage: [G_hi | G_lo | E_hi | E_lo], each 64 rows (the K axis:
+// rows q = b*S + s of this chunk) x 128 columns x 2 B = 256 B per row.  The
+// 32-B chunk c of row r sits at position c ^ (r & 7).  An MFMA fragment
+// (8 consecutive K rows of one column per lane) is two ds_read_b64_tr_b16;
+// within each K step the 32 rows are permuted so that a 32-lane half of one
+// transposed read touches rows 8j..8j+7 -> 8 distinct 32-B chunk positions,
+// all 64 banks once: conflict-free.  Element j of lane group g holds K row
+// 32*ks + (j < 4 ? 4g + j : 16 + 4g + j - 4), the same for A and B.
+struct Dr16Params {
+  const uint16_t* g_hi;
+  const uint16_t* g_lo;
+  const float* g_scale;
+  int64_t ldg;          // G plane row length (>= nLt*128)
+  mpv_split16 eps16;    // rows s*B + b, ld >= nZt*128
+  float* slab;          // [nKc][L][z]
+  int S, B, L, z;
+  int nLt, nZt, nKc, rows_per_chunk, rows_pad;
+};
+
+constexpr int kDrRowB = 256;  // bytes per LDS row (128 halves)
+constexpr int kDrKR = 64;     // K rows per chunk
+
+MPV_DEV void barrier_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+MPV_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+MPV_DEV s16x4 tr_read(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(base + off));
+}
+
+// block id -> (kc, tile): all tiles of one K chunk share rows -> ids equal mod 8
+MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
+  const int full = (K / 8) * 8 * nT;
+  if (id < full) {
+    const int q = id / (8 * nT), r = id % (8 * nT);
+    tile = r / 8;
+    kc = q * 8 + (r % 8);
+  } else {
+    const int r = id - full, Kr = K % 8;
+    tile = r / Kr;
+    kc = (K / 8) * 8 + (r % Kr);
+  }
+}
+
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(WM* WN * 64) void dR16_kernel(Dr16Params p) {
+  constexpr int NW = WM * WN;
+  constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
+  static_assert(BL == 128 && BZ == 128, "tile is 128 x 128 (one 256-B LDS row)");
+  constexpr int PLANE = kDrKR * kDrRowB;  // 16 KB
+  constexpr int STAGE = 4 * PLANE;
+  constexpr int GROUPS = STAGE / 1024;    // 64 wave-instructions (4 rows each)
+  static_assert(GROUPS % NW == 0, "DMA groups must split over waves");
+  constexpr int PER_WAVE = GROUPS / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  int kc, tile;
+  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
+  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, B = p.B, rows = B * S;
+  const int q_begin = kc * p.rows_per_chunk;
+  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
+  const int64_t lde = p.eps16.ld;
+  // DMA lane mapping: 4 rows of 256 B per 1-KB wave-instruction
+  const int dma_row = lane >> 4, dma_c = (lane & 15) >> 1, dma_half = lane & 1;
+  // transposed-read lane mapping: lane 4q+p of its 16-lane group
+  const int tq = lr >> 2, tp = lr & 3;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int stage, int q0) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int grp = wid * PER_WAVE + i;
+      const int plane = grp >> 4;                 // 16 groups (64 rows) per plane
+      const int r = ((grp & 15) << 2) + dma_row;  // K row within the chunk
+      const int c = dma_c ^ (r & 7);              // source 32-B chunk for this LDS slot
+      const int q = q0 + r;
+      const uint16_t* src;
+      if (plane < 2) {
+        src = (plane ? p.g_lo : p.g_hi) + (int64_t)q * p.ldg + l0;
+      } else {
+        const int qq = min(q, rows - 1);          // G rows >= rows are zero
+        const int bb = qq / S, s = qq - bb * S;
+        src = (plane == 3 ? p.eps16.lo : p.eps16.hi) + ((int64_t)s * B + bb) * lde + z0;
+      }
+      src += c * 16 + dma_half * 8;
+      __builtin_amdgcn_global_load_lds(
+          src, (__attribute__((address_space(3))) void*)(smem + stage * STAGE + grp * 1024), 16, 0,
+          0);
+    }
+  };
+
+  const int nchunk = (q_end - q_begin + kDrKR - 1) / kDrKR;
+  if (nchunk > 0) issue(0, q_begin);
+  for (int ci = 0; ci < nchunk; ++ci) {
+    const int cur = ci & 1;
+    if (ci + 1 < nchunk) {
+      issue(cur ^ 1, q_begin + (ci + 1) * kDrKR);
+      wait_vmcnt<PER_WAVE>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    barrier_raw();
+    const char* base = smem + cur * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      const int r0 = ks * 32 + lg * 4 + tq, r1 = r0 + 16;
+      const int sw = r0 & 7;  // == r1 & 7
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        const int cofs = (((wm * TM + m) ^ sw) << 5) + tp * 8;
+        const s16x4 h0 = tr_read(base, r0 * kDrRowB + cofs);
+        const s16x4 h1 = tr_read(base, r1 * kDrRowB + cofs);
+        const s16x4 l0v = tr_read(base + PLANE, r0 * kDrRowB + cofs);
+        const s16x4 l1v = tr_read(base + PLANE, r1 * kDrRowB + cofs);
+        ah[m] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        al[m] = __builtin_shufflevector(l0v, l1v, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int cofs = (((wn * TN + n) ^ sw) << 5) + tp * 8;
+        const s16x4 h0 = tr_read(base + 2 * PLANE, r0 * kDrRowB + cofs);
+        const s16x4 h1 = tr_read(base + 2 * PLANE, r1 * kDrRowB + cofs);
+        const s16x4 l0v = tr_read(base + 3 * PLANE, r0 * kDrRowB + cofs);
+        const s16x4 l1v = tr_read(base + 3 * PLANE, r1 * kDrRowB + cofs);
+        bh[n] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+        bl[n] = __builtin_shufflevector(l0v, l1v, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
+                                                             acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
+                                                             acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
+                                                             acc[m][n], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();
+  }
+  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
+  // D[i = l][j = z]: row = lg*4 + reg, col = lr
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = l0 + (wm * TM + m) * 16 + lg * 4 + i;
+        const int zc = z0 + (wn * TN + n) * 16 + lr;
+        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][i] * inv;
+      }
 }
 
 // ---------------------------------------------------------------- dR GEMM
@@ -330,16 +536,20 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
 
 // ------------------------------------------------------------------- plans
 struct BwdPlan {
-  int TPR, RPI, nLc, nSc, rows_per_chunk;
-  int nLt, nZt, nKc, dr_rows_per_chunk;
-  size_t coef_bytes, colpart_bytes, slab_bytes;
+  int TPR, RPI, nLc, nSc, rows_per_chunk;       // element pass
+  int nLt, nZt, nKc, dr_rows_per_chunk, rows_pad;  // dR GEMM
+  int64_t ldg;                                  // G plane row length (3xf16)
+  size_t coef_bytes, colpart_bytes, slab_bytes, bound_bytes, planes_bytes;
 };
 
-static BwdPlan plan_bwd(const mpv_shape* s) {
+static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   BwdPlan pl;
   const int64_t L = s->L, S = s->S_local, B = s->B, z = s->z;
-  pl.nLc = (int)cdiv(L, 1024);
-  pl.TPR = (int)(L >= 1024 ? 256 : cdiv(L, 4));
+  const bool planes = gemm == MPV_GEMM_F16X3;
+  pl.ldg = cdiv(L, 128) * 128;
+  const int64_t Lc = planes ? pl.ldg : L;  // columns the element pass covers
+  pl.nLc = (int)cdiv(Lc, 1024);
+  pl.TPR = (int)(Lc >= 1024 ? 256 : cdiv(Lc, 4));
   pl.RPI = 256 / pl.TPR;
   int64_t want = cdiv(2048, B * pl.nLc);
   if (want < 1) want = 1;
@@ -351,15 +561,19 @@ static BwdPlan plan_bwd(const mpv_shape* s) {
   pl.nZt = (int)cdiv(z, 128);
   const int64_t rows = B * S;
   const int64_t tiles = (int64_t)pl.nLt * pl.nZt;
+  const int64_t kr = planes ? 64 : 32;  // K rows per chunk of the GEMM
+  pl.rows_pad = (int)(cdiv(rows, kr) * kr);
   int64_t kc = cdiv(1536, tiles);
   const int64_t kc_max = cdiv(rows, 256);
   if (kc > kc_max) kc = kc_max;
   if (kc < 1) kc = 1;
-  pl.dr_rows_per_chunk = (int)(cdiv(cdiv(rows, kc), kDrBK) * kDrBK);
+  pl.dr_rows_per_chunk = (int)(cdiv(cdiv(rows, kc), kr) * kr);
   pl.nKc = (int)cdiv(rows, pl.dr_rows_per_chunk);
   pl.coef_bytes = align_up(sizeof(float) * 6 * (size_t)B * S, 256);
   pl.colpart_bytes = align_up(sizeof(float) * (size_t)pl.nSc * 2 * B * L, 256);
   pl.slab_bytes = align_up(sizeof(float) * (size_t)pl.nKc * L * z, 256);
+  pl.bound_bytes = align_up(sizeof(float) * ((size_t)B + 64), 256);
+  pl.planes_bytes = planes ? align_up(2 * sizeof(uint16_t) * (size_t)pl.rows_pad * pl.ldg, 256) : 0;
   return pl;
 }
 
@@ -369,19 +583,33 @@ using namespace mpv;
 
 extern "C" {
 
-size_t mpv_bwd_workspace_bytes(const mpv_shape* shape) {
+size_t mpv_bwd_workspace_bytes(const mpv_shape* shape, int gemm) {
   if (check_shape(shape) != MPV_OK) return 0;
-  const BwdPlan pl = plan_bwd(shape);
-  return pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes;
+  const BwdPlan pl = plan_bwd(shape, gemm);
+  return pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes + pl.bound_bytes + pl.planes_bytes;
 }
 
 int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) {
   if (int rc = check_shape(shape)) return rc;
-  MPV_REQUIRE(a && a->y && a->fe_out && a->fx_out && a->eps && a->T && a->rowstat && a->bstat &&
+  MPV_REQUIRE(a && a->y && a->fe_out && a->fx_out && a->T && a->rowstat && a->bstat &&
                   a->gscal && a->dfe_dfx && a->workspace,
               "NULL pointer in mpv_bwd_args");
-  const BwdPlan pl = plan_bwd(shape);
-  const size_t need = pl.coef_bytes + pl.colpart_bytes + (a->dR32 ? pl.slab_bytes : 0);
+  MPV_REQUIRE(a->gemm == MPV_GEMM_F32 || a->gemm == MPV_GEMM_F16X3, "unknown gemm mode %d",
+              a->gemm);
+  const bool planes = a->gemm == MPV_GEMM_F16X3;
+  const BwdPlan pl = plan_bwd(shape, a->gemm);
+  if (a->dR32) {
+    if (planes) {
+      MPV_REQUIRE(a->eps16.hi && a->eps16.lo && a->eps16.scale, "eps16 planes are NULL");
+      MPV_REQUIRE(a->eps16.ld >= (int64_t)pl.nZt * 128 && a->eps16.rows_pad >= shape->S_local * shape->B,
+                  "eps16 planes too small (ld %lld < %lld)", (long long)a->eps16.ld,
+                  (long long)pl.nZt * 128);
+    } else {
+      MPV_REQUIRE(a->eps != nullptr, "MPV_GEMM_F32 needs eps");
+    }
+  }
+  const size_t need = pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes + pl.bound_bytes +
+                      pl.planes_bytes;
   MPV_REQUIRE(a->workspace_bytes >= need, "workspace too small: %zu < %zu", a->workspace_bytes,
               need);
   hipStream_t st = as_stream(stream);
@@ -389,12 +617,28 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   float* coef = reinterpret_cast<float*>(ws);
   float* colpart = reinterpret_cast<float*>(ws + pl.coef_bytes);
   float* slab = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes);
+  float* gbound = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes);
+  float* gscale = gbound + shape->B;  // one float after the per-row bounds
+  uint16_t* g_hi = reinterpret_cast<uint16_t*>(ws + pl.coef_bytes + pl.colpart_bytes +
+                                               pl.slab_bytes + pl.bound_bytes);
+  uint16_t* g_lo = g_hi + (size_t)pl.rows_pad * pl.ldg;
   const int S = (int)shape->S_local, B = (int)shape->B, L = (int)shape->L, z = (int)shape->z;
+  const bool want_planes = planes && a->dR32 != nullptr;
 
   MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B), dim3(256), 0, st, a->y, a->rowstat, a->bstat,
-                     a->gscal, coef, S, B, L, (float)shape->S_total, a->nll_coeff, a->c_coeff,
-                     a->live);
+             a->gscal, a->g_indiv, a->g_indiv_label, coef, want_planes ? gbound : nullptr, S, B, L,
+             (float)shape->S_total, a->nll_coeff, a->c_coeff, a->live);
   if (int rc = check_launch("bwd_coef")) return rc;
+  if (want_planes) {
+    if (int rc = launch_scale(gbound, B, gscale, st)) return rc;
+    const int64_t pad_rows = (int64_t)pl.rows_pad - (int64_t)B * S;
+    if (pad_rows > 0) {
+      const size_t off = (size_t)B * S * pl.ldg, n = (size_t)pad_rows * pl.ldg * sizeof(uint16_t);
+      if (hipMemsetAsync(g_hi + off, 0, n, st) != hipSuccess ||
+          hipMemsetAsync(g_lo + off, 0, n, st) != hipSuccess)
+        return fail(MPV_ELAUNCH, "memset of G pad rows failed");
+    }
+  }
 
   ElemParams ep;
   ep.y = a->y;
@@ -404,38 +648,67 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.gIL = a->g_indiv_label;
   ep.coef = coef;
   ep.T = a->T;
+  ep.g_hi = want_planes ? g_hi : nullptr;
+  ep.g_lo = want_planes ? g_lo : nullptr;
+  ep.g_scale = gscale;
+  ep.ldg = pl.ldg;
   ep.colpart = colpart;
   ep.S = S;
   ep.B = B;
   ep.L = L;
+  ep.Lc = want_planes ? (int)pl.ldg : L;
   ep.TPR = pl.TPR;
   ep.RPI = pl.RPI;
   ep.rows_per_chunk = pl.rows_per_chunk;
   ep.inv_S = 1.0f / (float)shape->S_total;
   const dim3 eg(B, pl.nSc, pl.nLc);
-  if ((L & 3) == 0)
-    MPV_LAUNCH("bwd_elem", bwd_elem_kernel<true>, eg, dim3(256), 0, st, ep);
-  else
-    MPV_LAUNCH("bwd_elem", bwd_elem_kernel<false>, eg, dim3(256), 0, st, ep);
+  const bool vec = (L & 3) == 0;
+  if (want_planes) {
+    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true>), eg, dim3(256), 0, st, ep);
+    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, true>), eg, dim3(256), 0, st, ep);
+  } else {
+    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false>), eg, dim3(256), 0, st, ep);
+    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, false>), eg, dim3(256), 0, st, ep);
+  }
   if (int rc = check_launch("bwd_elem")) return rc;
   if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
     return rc;
 
   if (a->dR32) {
-    DrParams dp;
-    dp.G = a->T;
-    dp.eps = a->eps;
-    dp.slab = slab;
-    dp.S = S;
-    dp.B = B;
-    dp.L = L;
-    dp.z = z;
-    dp.nLt = pl.nLt;
-    dp.nZt = pl.nZt;
-    dp.nKc = pl.nKc;
-    dp.rows_per_chunk = pl.dr_rows_per_chunk;
     const int64_t blocks = (int64_t)pl.nLt * pl.nZt * pl.nKc;
-    MPV_LAUNCH("dR_gemm", (dR_gemm_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+    if (planes) {
+      Dr16Params dp;
+      dp.g_hi = g_hi;
+      dp.g_lo = g_lo;
+      dp.g_scale = gscale;
+      dp.ldg = pl.ldg;
+      dp.eps16 = a->eps16;
+      dp.slab = slab;
+      dp.S = S;
+      dp.B = B;
+      dp.L = L;
+      dp.z = z;
+      dp.nLt = pl.nLt;
+      dp.nZt = pl.nZt;
+      dp.nKc = pl.nKc;
+      dp.rows_per_chunk = pl.dr_rows_per_chunk;
+      dp.rows_pad = pl.rows_pad;
+      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+    } else {
+      DrParams dp;
+      dp.G = a->T;
+      dp.eps = a->eps;
+      dp.slab = slab;
+      dp.S = S;
+      dp.B = B;
+      dp.L = L;
+      dp.z = z;
+      dp.nLt = pl.nLt;
+      dp.nZt = pl.nZt;
+      dp.nKc = pl.nKc;
+      dp.rows_per_chunk = pl.dr_rows_per_chunk;
+      MPV_LAUNCH("dR_gemm", (dR_gemm_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+    }
     if (int rc = check_launch("dR_gemm")) return rc;
     if (int rc = launch_sum_slabs(slab, pl.nKc, (int64_t)L * z, a->dR32, MPV_F32, st)) return rc;
   }

@@ -1,22 +1,26 @@
 // Forward of the MPVAE probit ELBO for one S-shard (reference mpvae.py:145-210).
 //
-//   probit_fwd_kernel  t = eps . R^T on the fp32 matrix cores
-//                      (v_mfma_f32_16x16x4_f32, exact f32 fmas), fused epilogue:
-//                      u = t + fe_out / fx_out, E = Phi(u)(1-1e-6)+0.5e-6 for both
-//                      branches, per-row BCE log-prob and ranking factors P, N
-//                      (partial over this column tile), column sums of E over s,
-//                      optional T stash for the backward.
-//   fwd_combine_kernel one block per batch row b: sums the column-tile
-//                      partials, writes rowstat, the shard's log-sum-exp stats
-//                      (m, Z) and ranking sums.
-//   finalize_kernel    the 8 outputs of compute_loss (+ KL, mpvae.py:147-148).
+//   probit_fwd16_kernel  t = eps . R^T with 3xf16 split operands on the f16
+//                        matrix cores (v_mfma_f32_16x16x32_f16, fp32 accumulate,
+//                        ~fp32 accuracy, see mpv_common.h), operand tiles
+//                        streamed global->LDS by LDS-DMA (global_load_lds_dwordx4)
+//                        into a double-buffered, XOR-swizzled image.
+//   probit_fwd_kernel    the same with exact fp32 MFMA (v_mfma_f32_16x16x4_f32)
+//                        on fp32 operands (MPV_GEMM_F32, the bit-faithful mode).
+//   Both share the fused epilogue: u = t + fe_out / fx_out,
+//   E = Phi(u)(1-1e-6)+0.5e-6 for both branches, per-row BCE log-prob and
+//   ranking factors P, N (partial over this label tile), column sums of E over
+//   s, optional T stash for the backward.
+//   fwd_combine_kernel   one block per batch row b: sums the label-tile
+//                        partials, writes rowstat, the shard's log-sum-exp
+//                        statistics (m, Z) and ranking sums.
+//   finalize_kernel      the 8 outputs of compute_loss (+ KL, mpvae.py:147-148).
 //
-// Tiling: a workgroup owns one batch row b, one column tile [n0, n0+BN) of the
-// labels and a chunk of s-tiles of BM samples; the M axis of the GEMM is s
-// (rows of eps for fixed b), so the fe/fx/y values of the epilogue are
-// per-lane constants and the column sums over s never leave registers until
-// the workgroup ends.  Workgroups that share the same eps rows (same b, same
-// s-chunk, different column tiles) are numbered so they land on one XCD.
+// Tiling: a workgroup owns one batch row b, one label tile [n0, n0+BN) and a
+// chunk of s-tiles of BM samples; the GEMM's M axis is s (eps rows for fixed
+// b), so fe/fx/y of the epilogue are per-lane constants and the column sums
+// over s stay in registers until the workgroup ends.  Workgroups sharing eps
+// rows (same b and s-chunk, other label tiles) get ids equal mod 8: one XCD.
 #include "abi_util.h"
 #include "mpv_common.h"
 
@@ -29,8 +33,10 @@ struct FwdParams {
   const float* y;
   const float* fe;
   const float* fx;
-  const float* R;
-  const float* eps;
+  const float* R;    // fp32 mode
+  const float* eps;  // fp32 mode
+  mpv_split16 R16;   // 3xf16 mode
+  mpv_split16 eps16;
   float* T;
   float* rowpart;  // [6][nNt][B][S]
   float* colpart;  // [nSc][2][B][L]
@@ -38,10 +44,10 @@ struct FwdParams {
   int nNt, nSc, tps, nSt;
 };
 
-constexpr int kBK = 32;   // K (= z) chunk staged in LDS
-constexpr int kLDK = 40;  // LDS row stride in floats: conflict-free ds_read_b128
+constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
+constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
 
-// Block id -> (group g = b*nSc + sc, column tile nt).  All nNt tiles of one
+// Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
 MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
   const int full = (G / 8) * 8 * nNt;
@@ -56,6 +62,144 @@ MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
   }
 }
 
+// ------------------------------------------------------------ shared epilogue
+// Per-lane constants of the label columns this lane owns (MFMA C layout:
+// col = lane & 15 within each 16-wide tile), and its running column sums.
+template <int TN>
+struct FwdLane {
+  float fe[TN], fx[TN], y[TN], colE[TN], colEx[TN];
+  int col[TN];
+  bool colok[TN], soft[TN];
+};
+
+template <int WN, int TN>
+MPV_DEV void fwd_lane_init(FwdLane<TN>& ln, const FwdParams& p, int b, int n0, int wn, int lr) {
+#pragma unroll
+  for (int n = 0; n < TN; ++n) {
+    const int col = n0 + wn * TN * 16 + n * 16 + lr;
+    ln.col[n] = col;
+    ln.colok[n] = col < p.L;
+    const int64_t o = (int64_t)b * p.L + (ln.colok[n] ? col : 0);
+    ln.y[n] = ln.colok[n] ? p.y[o] : 0.0f;
+    ln.fe[n] = ln.colok[n] ? p.fe[o] : 0.0f;
+    ln.fx[n] = ln.colok[n] ? p.fx[o] : 0.0f;
+    ln.soft[n] = !(ln.y[n] == 0.0f || ln.y[n] == 1.0f);
+    ln.colE[n] = ln.colEx[n] = 0.0f;
+  }
+}
+
+// One BM x BN tile of t (acc * scale): probit decode, row statistics written
+// to rowpart[., nt, b, s], column sums accumulated in `ln`.  Called by every
+// thread of the workgroup; uses `smem` (>= WN*BM*6 floats) after a barrier.
+template <int WM, int WN, int TM, int TN>
+MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)[TM][TN],
+                               float scale, int b, int s0, int nt, float* smem) {
+  constexpr int NT = WM * WN * 64, BM = WM * TM * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN, lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, B = p.B, L = p.L;
+  float* red = smem;  // [WN][BM][6]
+  __syncthreads();    // the main loop's last LDS reads are done before red is written
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wm * TM * 16 + m * 16 + lg * 4 + i;
+      const int s = s0 + rl;
+      const bool rowok = s < S;
+      float st6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const bool ok = rowok && ln.colok[n];
+        const float t = acc[m][n][i] * scale;
+        if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + ln.col[n]] = t;
+        const float E = probit_prob(t + ln.fe[n]);
+        const float Ex = probit_prob(t + ln.fx[n]);
+        const float y = ln.y[n];
+        // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
+        float le = logf(y == 0.0f ? 1.0f - E : E);
+        float lx = logf(y == 0.0f ? 1.0f - Ex : Ex);
+        if (ln.soft[n]) {
+          le = y * logf(E) + (1.0f - y) * logf(1.0f - E);
+          lx = y * logf(Ex) + (1.0f - y) * logf(1.0f - Ex);
+        }
+        // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
+        const float sg = (y == 1.0f) ? -5.0f : 5.0f;
+        const float re = expf(sg * E), rx = expf(sg * Ex);
+        const float wpos = (ok && y == 1.0f) ? 1.0f : 0.0f;
+        const float wneg = (ok && y == 0.0f) ? 1.0f : 0.0f;
+        st6[0] += ok ? le : 0.0f;
+        st6[1] += ok ? lx : 0.0f;
+        st6[2] += wpos * re;
+        st6[3] += wneg * re;
+        st6[4] += wpos * rx;
+        st6[5] += wneg * rx;
+        ln.colE[n] += rowok ? E : 0.0f;
+        ln.colEx[n] += rowok ? Ex : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) st6[k] = row16_sum_to_lane15(st6[k]);
+      if (lr == 15) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[(wn * BM + rl) * 6 + k] = st6[k];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one m-slab
+  }
+  __syncthreads();
+  for (int r = tid; r < BM; r += NT) {
+    const int s = s0 + r;
+    if (s < S) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < WN; ++w) v += red[(w * BM + r) * 6 + k];
+        p.rowpart[(((int64_t)k * p.nNt + nt) * B + b) * S + s] = v;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Column sums of this workgroup -> colpart[sc, ., b, n0 ...].
+template <int WM, int WN, int TM, int TN>
+MPV_DEV void fwd_colsum_epilogue(const FwdParams& p, FwdLane<TN>& ln, int b, int sc, int n0,
+                                 float* smem) {
+  constexpr int NT = WM * WN * 64, BN = WN * TN * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN, lr = lane & 15, lg = lane >> 4;
+  float* cred = smem;  // [WM][BN][2]
+#pragma unroll
+  for (int n = 0; n < TN; ++n) {
+    float e = ln.colE[n], x = ln.colEx[n];
+    e += __shfl_xor(e, 16, 64);
+    e += __shfl_xor(e, 32, 64);
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    if (lg == 0) {
+      const int cl = wn * TN * 16 + n * 16 + lr;
+      cred[(wm * BN + cl) * 2 + 0] = e;
+      cred[(wm * BN + cl) * 2 + 1] = x;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < BN; c += NT) {
+    const int col = n0 + c;
+    if (col < p.L) {
+      float e = 0.f, x = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        e += cred[(w * BN + c) * 2 + 0];
+        x += cred[(w * BN + c) * 2 + 1];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + col] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + col] = x;
+    }
+  }
+}
+
+// ------------------------------------------------------ exact fp32 mainloop
 template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
   constexpr int NT = WM * WN * 64;
@@ -79,24 +223,8 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
   const int S = p.S, B = p.B, L = p.L, z = p.z;
   const bool zvec = (z & 3) == 0;
 
-  // per-lane column constants (fixed b)
-  float fe_c[TN], fx_c[TN], y_c[TN];
-  bool colok[TN], soft[TN];
-  int col_c[TN];
-#pragma unroll
-  for (int n = 0; n < TN; ++n) {
-    const int col = n0 + wn * TN * 16 + n * 16 + lr;
-    col_c[n] = col;
-    colok[n] = col < L;
-    const int64_t o = (int64_t)b * L + (colok[n] ? col : 0);
-    y_c[n] = colok[n] ? p.y[o] : 0.0f;
-    fe_c[n] = colok[n] ? p.fe[o] : 0.0f;
-    fx_c[n] = colok[n] ? p.fx[o] : 0.0f;
-    soft[n] = !(y_c[n] == 0.0f || y_c[n] == 1.0f);
-  }
-  float colE[TN], colEx[TN];
-#pragma unroll
-  for (int n = 0; n < TN; ++n) colE[n] = colEx[n] = 0.0f;
+  FwdLane<TN> ln;
+  fwd_lane_init<WN, TN>(ln, p, b, n0, wn, lr);
 
   const int nK = (z + kBK - 1) / kBK;
   const int st_end = min(p.nSt, (sc + 1) * p.tps);
@@ -196,99 +324,142 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
         __syncthreads();
       }
     }
+    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, 1.0f, b, s0, nt, smem);
+  }
+  fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, smem);
+}
 
-    // ---- epilogue: probit decode + row statistics + column sums
-    float* red = smem;  // [WN][BM][6]
+// ------------------------------------------------------ 3xf16 mainloop
+// LDS image per stage: [A_hi | A_lo | B_hi | B_lo], each row 128 B = 64 halves
+// of one K chunk.  A 16-B chunk c of row r sits at position c ^ ((r >> 1) & 7):
+// the ds_read_b128 fragment reads (16 rows x one 16-B column per lane group)
+// then hit 16 distinct slots of the 256-B bank row (checked by script, see
+// DESIGN.md).  LDS-DMA writes lane-linearly, so the swizzle is applied to the
+// per-lane SOURCE address and undone by the same XOR on the read.
+constexpr int kRowB = 128;  // bytes per plane row per K chunk (64 halves)
+
+MPV_DEV void barrier_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+MPV_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WM, int WN, int TM, int TN, int NSTAGE>
+__global__ __launch_bounds__(WM* WN * 64) void probit_fwd16_kernel(FwdParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+  constexpr int PLANE_A = BM * kRowB, PLANE_B = BN * kRowB;
+  constexpr int STAGE = 2 * PLANE_A + 2 * PLANE_B;
+  constexpr int GROUPS = STAGE / 1024;  // 1-KB LDS-DMA wave-instructions per stage
+  static_assert(STAGE % 1024 == 0 && GROUPS % NW == 0, "DMA groups must split over waves");
+  constexpr int PER_WAVE = GROUPS / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, B = p.B;
+  const int64_t lda = p.eps16.ld, ldb = p.R16.ld;
+
+  FwdLane<TN> ln;
+  fwd_lane_init<WN, TN>(ln, p, b, n0, wn, lr);
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + 63) / 64;
+  const int sw_r = (lr >> 1) & 7;        // swizzle of every fragment row this lane reads
+  const int dma_row = lane >> 3;         // row within a 1-KB group
+  const int dma_pos = lane & 7;          // 16-B position within the row
+
+  const int st_end = min(p.nSt, (sc + 1) * p.tps);
+  for (int st = sc * p.tps; st < st_end; ++st) {
+    const int s0 = st * BM;
+    // issue one K chunk of all four planes into `stage`
+    auto issue = [&](int stage, int k0) {
 #pragma unroll
-    for (int m = 0; m < TM; ++m) {
+      for (int i = 0; i < PER_WAVE; ++i) {
+        const int grp = wid * PER_WAVE + i;
+        const int row = grp * 8 + dma_row;  // row in the concatenated planes
+        const uint16_t* src;
+        int r;
+        if (row < 2 * BM) {
+          const int plane = row >= BM;
+          r = row - plane * BM;
+          const int s = min(s0 + r, S - 1);
+          src = (plane ? p.eps16.lo : p.eps16.hi) + ((int64_t)s * B + b) * lda + k0;
+        } else {
+          const int plane = row >= 2 * BM + BN;
+          r = row - 2 * BM - plane * BN;
+          src = (plane ? p.R16.lo : p.R16.hi) + (int64_t)(n0 + r) * ldb + k0;
+        }
+        src += (dma_pos ^ ((r >> 1) & 7)) * 8;
+        __builtin_amdgcn_global_load_lds(
+            src, (__attribute__((address_space(3))) void*)(smem + stage * STAGE + grp * 1024), 16,
+            0, 0);
+      }
+    };
+
+    f32x4 acc[TM][TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = wm * TM * 16 + m * 16 + lg * 4 + i;
-        const int s = s0 + rl;
-        const bool rowok = s < S;
-        float st6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue(0, 0);
+    for (int kc = 0; kc < nK; ++kc) {
+      const int cur = NSTAGE == 2 ? (kc & 1) : 0;
+      if (NSTAGE == 2 && kc + 1 < nK) {
+        issue(cur ^ 1, (kc + 1) * 64);
+        wait_vmcnt<PER_WAVE>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      barrier_raw();
+      const char* base = smem + cur * STAGE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int coff = (((4 * ks + lg) ^ sw_r) << 4);
+        s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          const int off = ((wm * TM + m) * 16 + lr) * kRowB + coff;
+          ah[m] = *reinterpret_cast<const s16x8*>(base + off);
+          al[m] = *reinterpret_cast<const s16x8*>(base + PLANE_A + off);
+        }
 #pragma unroll
         for (int n = 0; n < TN; ++n) {
-          const bool ok = rowok && colok[n];
-          const float t = acc[m][n][i];
-          if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + col_c[n]] = t;
-          const float E = probit_prob(t + fe_c[n]);
-          const float Ex = probit_prob(t + fx_c[n]);
-          const float y = y_c[n];
-          // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
-          float le = logf(y == 0.0f ? 1.0f - E : E);
-          float lx = logf(y == 0.0f ? 1.0f - Ex : Ex);
-          if (soft[n]) {
-            le = y * logf(E) + (1.0f - y) * logf(1.0f - E);
-            lx = y * logf(Ex) + (1.0f - y) * logf(1.0f - Ex);
+          const int off = 2 * PLANE_A + ((wn * TN + n) * 16 + lr) * kRowB + coff;
+          bh[n] = *reinterpret_cast<const s16x8*>(base + off);
+          bl[n] = *reinterpret_cast<const s16x8*>(base + PLANE_B + off);
+        }
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
+                                                               acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
+                                                               acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
+                                                               acc[m][n], 0, 0, 0);
           }
-          // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-          const float sg = (y == 1.0f) ? -5.0f : 5.0f;
-          const float re = expf(sg * E), rx = expf(sg * Ex);
-          const float wpos = (ok && y == 1.0f) ? 1.0f : 0.0f;
-          const float wneg = (ok && y == 0.0f) ? 1.0f : 0.0f;
-          st6[0] += ok ? le : 0.0f;
-          st6[1] += ok ? lx : 0.0f;
-          st6[2] += wpos * re;
-          st6[3] += wneg * re;
-          st6[4] += wpos * rx;
-          st6[5] += wneg * rx;
-          colE[n] += rowok ? E : 0.0f;
-          colEx[n] += rowok ? Ex : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < 6; ++k) st6[k] = row16_sum_to_lane15(st6[k]);
-        if (lr == 15) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) red[(wn * BM + rl) * 6 + k] = st6[k];
-        }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();
+      if (NSTAGE == 1 && kc + 1 < nK) issue(0, (kc + 1) * 64);
     }
-    __syncthreads();
-    for (int r = tid; r < BM; r += NT) {
-      const int s = s0 + r;
-      if (s < S) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          float v = 0.0f;
-#pragma unroll
-          for (int w = 0; w < WN; ++w) v += red[(w * BM + r) * 6 + k];
-          p.rowpart[(((int64_t)k * p.nNt + nt) * B + b) * S + s] = v;
-        }
-      }
-    }
-    __syncthreads();
+    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, nt,
+                                      reinterpret_cast<float*>(smem));
   }
-
-  // ---- column sums over this workgroup's samples
-  float* cred = smem;  // [WM][BN][2]
-#pragma unroll
-  for (int n = 0; n < TN; ++n) {
-    float e = colE[n], x = colEx[n];
-    e += __shfl_xor(e, 16, 64);
-    e += __shfl_xor(e, 32, 64);
-    x += __shfl_xor(x, 16, 64);
-    x += __shfl_xor(x, 32, 64);
-    if (lg == 0) {
-      const int cl = wn * TN * 16 + n * 16 + lr;
-      cred[(wm * BN + cl) * 2 + 0] = e;
-      cred[(wm * BN + cl) * 2 + 1] = x;
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < BN; c += NT) {
-    const int col = n0 + c;
-    if (col < L) {
-      float e = 0.f, x = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        e += cred[(w * BN + c) * 2 + 0];
-        x += cred[(w * BN + c) * 2 + 1];
-      }
-      p.colpart[(((int64_t)sc * 2 + 0) * B + b) * L + col] = e;
-      p.colpart[(((int64_t)sc * 2 + 1) * B + b) * L + col] = x;
-    }
-  }
+  fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, reinterpret_cast<float*>(smem));
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
@@ -398,7 +569,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(mpv_final_args a, int B, 
 
 // ---------------------------------------------------------------- host side
 struct FwdPlan {
-  int cfg;  // 0: 4x1 waves TM2 TN3 (BN 48); 1: 4x1 TM2 TN6 (BN 96); 2: 2x2 TM4 TN4 (BN 128)
+  int cfg;  // tile configuration, see launch_fwd
   int BM, BN, nNt, nSt, nSc, tps;
   size_t rowpart_bytes, colpart_bytes;
 };
@@ -421,6 +592,44 @@ static FwdPlan plan_fwd(const mpv_shape* s) {
   return pl;
 }
 
+static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, const FwdParams& p) {
+  if (gemm == MPV_GEMM_F32) {
+    switch (pl.cfg) {
+      case 0:
+        MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<4, 1, 2, 3>), grid, dim3(256), 0, st, p);
+        break;
+      case 1:
+        MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<4, 1, 2, 6>), grid, dim3(256), 0, st, p);
+        break;
+      default:
+        MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<2, 2, 4, 4>), grid, dim3(256), 0, st, p);
+        break;
+    }
+  } else {
+    switch (pl.cfg) {
+      case 0:  // BN 48, 4 waves, single-buffered (44 KB LDS: 3 workgroups per CU)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 1>), grid, dim3(256), 0, st, p);
+        break;
+      case 1:  // BN 96, 8 waves, double-buffered (112 KB)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 2>), grid, dim3(512), 0, st, p);
+        break;
+      default:  // BN 128, 8 waves, double-buffered (128 KB)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<2, 4, 4, 2, 2>), grid, dim3(512), 0, st, p);
+        break;
+    }
+  }
+}
+
+static int check_split_operand(const mpv_split16& o, int64_t rows, int64_t ld_min,
+                               const char* what) {
+  MPV_REQUIRE(o.hi && o.lo && o.scale, "%s: NULL plane", what);
+  MPV_REQUIRE(o.rows_pad >= rows, "%s: rows_pad %lld < %lld", what, (long long)o.rows_pad,
+              (long long)rows);
+  MPV_REQUIRE(o.ld >= ld_min && (o.ld % 8) == 0, "%s: ld %lld must be >= %lld and a multiple of 8",
+              what, (long long)o.ld, (long long)ld_min);
+  return MPV_OK;
+}
+
 }  // namespace mpv
 
 using namespace mpv;
@@ -436,10 +645,19 @@ size_t mpv_fwd_workspace_bytes(const mpv_shape* shape) {
 int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) {
   if (int rc = check_shape(shape)) return rc;
   MPV_REQUIRE(a != nullptr, "args is NULL");
-  MPV_REQUIRE(a->y && a->fe_out && a->fx_out && a->R32 && a->eps && a->rowstat && a->bstat &&
-                  a->colsum && a->workspace,
+  MPV_REQUIRE(a->y && a->fe_out && a->fx_out && a->rowstat && a->bstat && a->colsum &&
+                  a->workspace,
               "NULL pointer in mpv_fwd_args");
+  MPV_REQUIRE(a->gemm == MPV_GEMM_F32 || a->gemm == MPV_GEMM_F16X3, "unknown gemm mode %d",
+              a->gemm);
   const FwdPlan pl = plan_fwd(shape);
+  if (a->gemm == MPV_GEMM_F32) {
+    MPV_REQUIRE(a->R32 && a->eps, "MPV_GEMM_F32 needs R32 and eps");
+  } else {
+    const int64_t zp = cdiv(shape->z, 64) * 64;
+    if (int rc = check_split_operand(a->R16, (int64_t)pl.nNt * pl.BN, zp, "R16")) return rc;
+    if (int rc = check_split_operand(a->eps16, shape->S_local * shape->B, zp, "eps16")) return rc;
+  }
   MPV_REQUIRE(a->workspace_bytes >= pl.rowpart_bytes + pl.colpart_bytes,
               "workspace too small: %zu < %zu", a->workspace_bytes,
               pl.rowpart_bytes + pl.colpart_bytes);
@@ -450,6 +668,8 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   p.fx = a->fx_out;
   p.R = a->R32;
   p.eps = a->eps;
+  p.R16 = a->R16;
+  p.eps16 = a->eps16;
   p.T = a->T;
   p.rowpart = reinterpret_cast<float*>(a->workspace);
   p.colpart = pl.nSc > 1 ? reinterpret_cast<float*>((char*)a->workspace + pl.rowpart_bytes)
@@ -464,20 +684,10 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   p.nSt = pl.nSt;
   const int64_t blocks = (int64_t)shape->B * pl.nSc * pl.nNt;
   MPV_REQUIRE(blocks < (int64_t(1) << 31), "grid too large");
-  switch (pl.cfg) {
-    case 0:
-      MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<4, 1, 2, 3>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-      break;
-    case 1:
-      MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<4, 1, 2, 6>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-      break;
-    default:
-      MPV_LAUNCH("probit_fwd", (probit_fwd_kernel<2, 2, 4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, p);
-      break;
-  }
+  launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
   MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(256), 0, st, a->y,
-                     p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
+             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
   if (int rc = check_launch("fwd_combine")) return rc;
   if (pl.nSc > 1) {
     if (int rc = launch_sum_slabs(p.colpart, pl.nSc, 2 * shape->B * shape->L, a->colsum, MPV_F32, st))
@@ -495,8 +705,8 @@ int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* a, void* s
   const int64_t n = shape->B * shape->L;
   int64_t nb = cdiv(n, 256);
   if (nb > 4096) nb = 4096;
-  MPV_LAUNCH("finalize", finalize_kernel, dim3((unsigned)(1 + nb)), dim3(256), 0, as_stream(stream),
-                     *a, (int)shape->B, (int)shape->L, (float)shape->S_total);
+  MPV_LAUNCH("finalize", finalize_kernel, dim3((unsigned)(1 + nb)), dim3(256), 0,
+             as_stream(stream), *a, (int)shape->B, (int)shape->L, (float)shape->S_total);
   return check_launch("finalize");
 }
 

@@ -210,6 +210,91 @@ __global__ void kl_bwd_kernel(mpv_kl_bwd_args a) {
   }
 }
 
+// --------------------------------------------------------- 3xf16 operands
+constexpr int kMaxBlocks = 1024;  // block maxima of maxabs_kernel
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxabs_kernel(const T* __restrict__ x, int64_t n,
+                                                    float* __restrict__ block_max) {
+  __shared__ float red[16];
+  float m = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf((float)x[i]));
+  m = block_reduce<true>(m, red);
+  if (threadIdx.x == 0) block_max[blockIdx.x] = m;
+}
+
+// scale = pow2_scale(max of n block maxima) [* extra bound factor]
+__global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ block_max, int n,
+                                                   float* __restrict__ scale) {
+  __shared__ float red[16];
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, block_max[i]);
+  m = block_reduce<true>(m, red);
+  if (threadIdx.x == 0) *scale = pow2_scale(m);
+}
+
+// (rows, cols) row-major -> hi/lo planes (rows_pad, ld), zero padded.
+template <typename T>
+__global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int64_t rows,
+                                                   int64_t cols, mpv_split16 out) {
+  const float s = *out.scale;
+  const int64_t n = out.rows_pad * out.ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / out.ld, c = i - r * out.ld;
+    const float v = (r < rows && c < cols) ? (float)x[r * cols + c] : 0.0f;
+    uint16_t h, l;
+    split_f16(v, s, h, l);
+    out.hi[i] = h;
+    out.lo[i] = l;
+  }
+}
+
+// Philox noise straight into 3xf16 planes: row = s*B + b (padded to ld).
+// Box-Muller output is bounded by sqrt(-2 ln 2^-25) < 5.9, so the scale is
+// the constant 2^12 (max |n| * s < 24200 < 65504).
+constexpr float kNoiseScale = 4096.0f;
+
+__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int64_t rows,
+                                                            int64_t z, int64_t e_row0,
+                                                            uint32_t k0, uint32_t k1,
+                                                            uint64_t offset) {
+  const int64_t q4 = out.ld >> 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * q4) return;
+  const int64_t r = i / q4, c0 = (i - r * q4) * 4;
+  uint64_t cached = ~0ull;
+  u32x4 w = {0u, 0u, 0u, 0u};
+  uint16_t h[4], l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t c = c0 + q;
+    float v = 0.0f;
+    if (c < z) {
+      const int64_t e = (e_row0 + r) * z + c;  // global element index
+      const uint64_t g = (uint64_t)(e >> 2);
+      if (g != cached) {
+        const uint64_t ctr = g + offset;
+        w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+        cached = g;
+      }
+      float n0, n1;
+      const int ln = (int)(e & 3);
+      if (ln < 2) box_muller(w.x, w.y, n0, n1);
+      else box_muller(w.z, w.w, n0, n1);
+      v = (ln & 1) ? n1 : n0;
+    }
+    split_f16(v, kNoiseScale, h[q], l[q]);
+  }
+  const int64_t o = r * out.ld + c0;
+  *reinterpret_cast<s16x4*>(out.hi + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+  *reinterpret_cast<s16x4*>(out.lo + o) = s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+}
+
+__global__ void set_scalar_kernel(float* p, float v) { *p = v; }
+
 static unsigned grid_for(int64_t n, int threads, int64_t cap = 65536) {
   int64_t g = cdiv(n, threads);
   if (g > cap) g = cap;
@@ -283,6 +368,56 @@ int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* 
   return check_launch("philox_raw");
 }
 
+static int check_split(const mpv_split16* o) {
+  MPV_REQUIRE(o && o->hi && o->lo && o->scale, "NULL pointer in mpv_split16");
+  MPV_REQUIRE(o->rows_pad > 0 && o->ld > 0 && (o->ld % 8) == 0, "mpv_split16: ld must be a "
+              "positive multiple of 8 (got %lld)", (long long)o->ld);
+  return MPV_OK;
+}
+
+size_t mpv_split_workspace_bytes(void) { return sizeof(float) * kMaxBlocks; }
+
+int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const mpv_split16* out,
+                  void* workspace, void* stream) {
+  if (int rc = check_split(out)) return rc;
+  MPV_REQUIRE(x && workspace && rows > 0 && cols > 0, "bad mpv_split_f16 arguments");
+  MPV_REQUIRE(rows <= out->rows_pad && cols <= out->ld, "planes smaller than the input");
+  MPV_REQUIRE(x_dtype == MPV_F32 || x_dtype == MPV_F64, "unsupported dtype %d", x_dtype);
+  hipStream_t s = as_stream(stream);
+  float* bmax = reinterpret_cast<float*>(workspace);
+  const int64_t n = rows * cols;
+  const unsigned g = grid_for(n, 256, kMaxBlocks);
+  if (x_dtype == MPV_F64)
+    MPV_LAUNCH("split", maxabs_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)x, n, bmax);
+  else
+    MPV_LAUNCH("split", maxabs_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, n, bmax);
+  MPV_LAUNCH("split", scale_kernel, dim3(1), dim3(256), 0, s, bmax, (int)g, out->scale);
+  const unsigned g2 = grid_for(out->rows_pad * out->ld, 256, 16384);
+  if (x_dtype == MPV_F64)
+    MPV_LAUNCH("split", split_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)x, rows,
+               cols, *out);
+  else
+    MPV_LAUNCH("split", split_kernel<float>, dim3(g2), dim3(256), 0, s, (const float*)x, rows,
+               cols, *out);
+  return check_launch("split_f16");
+}
+
+int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                         const mpv_split16* out, void* stream) {
+  if (int rc = check_shape(shape)) return rc;
+  if (int rc = check_split(out)) return rc;
+  const int64_t rows = shape->S_local * shape->B;
+  MPV_REQUIRE(out->rows_pad >= rows && out->ld >= shape->z, "noise planes too small");
+  hipStream_t s = as_stream(stream);
+  MPV_LAUNCH("noise_philox", set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
+  const int64_t n = rows * (out->ld / 4);
+  MPV_REQUIRE(cdiv(n, 256) < (int64_t(1) << 31), "noise too large");
+  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
+             *out, rows, shape->z, shape->s_offset * shape->B, (uint32_t)seed,
+             (uint32_t)(seed >> 32), offset);
+  return check_launch("noise_philox_f16");
+}
+
 int mpv_convert(const void* src, int sd, void* dst, int dd, int64_t n, void* stream) {
   MPV_REQUIRE(src && dst && n >= 0, "bad convert arguments");
   MPV_REQUIRE((sd == MPV_F32 || sd == MPV_F64) && (dd == MPV_F32 || dd == MPV_F64),
@@ -351,6 +486,11 @@ int mpv_kl_bwd(const mpv_kl_bwd_args* a, void* stream) {
 
 namespace mpv {
 // Used by the forward / backward translation units.
+int launch_scale(const float* block_max, int n, float* scale, hipStream_t s) {
+  MPV_LAUNCH("bwd_coef", scale_kernel, dim3(1), dim3(256), 0, s, block_max, n, scale);
+  return check_launch("scale");
+}
+
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
                      hipStream_t s) {
   const unsigned g = grid_for(n, 256, 8192);

@@ -24,6 +24,9 @@ Build-only knobs read from ``args`` (defaults reproduce the reference):
                a (n_sample, B, z_dim) float32 tensor: use it as the noise.
   mpvae_seed   philox seed (default: drawn from torch's CPU generator, so
                runs are reproducible under torch.manual_seed).
+  mpvae_gemm   "f16x3" (default): noise GEMMs on the f16 matrix cores with
+               3xf16 split operands (~fp32 accuracy, DESIGN.md section 4);
+               "f32": exact fp32 matrix-core GEMMs.
   mpvae_shard  True: shard the n_sample axis over the default
                torch.distributed group (mpvae_dist.py); default False.
 """
@@ -171,6 +174,6 @@ def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar
     shard = mpvae_dist.shard_for(args, n_sample)
     noise, kw = _noise_source(args, n_sample, B, z, shard, fe_out.device)
     cfg = ElboConfig(n_sample, shard.S_local, shard.s_offset, args.nll_coeff, args.c_coeff,
-                     exchange=shard.exchange, **kw)
+                     exchange=shard.exchange, gemm=getattr(args, "mpvae_gemm", "f16x3"), **kw)
     return ProbitELBO.apply(input_label.float(), fe_out, fe_mu, fe_logvar, fx_out, fx_mu,
                             fx_logvar, r_sqrt_sigma, noise, cfg)

@@ -31,9 +31,18 @@ class Shape(ctypes.Structure):
                 ("z", ctypes.c_int64)]
 
 
+class Split16(ctypes.Structure):
+    _fields_ = [("hi", vp), ("lo", vp), ("scale", vp), ("rows_pad", ctypes.c_int64),
+                ("ld", ctypes.c_int64)]
+
+
+GEMM_F16X3, GEMM_F32 = 0, 1
+
+
 class FwdArgs(ctypes.Structure):
-    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("R32", vp), ("eps", vp), ("T", vp),
-                ("rowstat", vp), ("bstat", vp), ("colsum", vp), ("workspace", vp),
+    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("gemm", ctypes.c_int), ("R32", vp),
+                ("eps", vp), ("R16", Split16), ("eps16", Split16), ("T", vp), ("rowstat", vp),
+                ("bstat", vp), ("colsum", vp), ("workspace", vp),
                 ("workspace_bytes", ctypes.c_size_t)]
 
 
@@ -46,7 +55,8 @@ class FinalArgs(ctypes.Structure):
 
 
 class BwdArgs(ctypes.Structure):
-    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("eps", vp), ("T", vp),
+    _fields_ = [("y", vp), ("fe_out", vp), ("fx_out", vp), ("gemm", ctypes.c_int), ("eps", vp),
+                ("eps16", Split16), ("T", vp),
                 ("rowstat", vp), ("bstat", vp), ("gscal", vp), ("g_indiv", vp),
                 ("g_indiv_label", vp), ("nll_coeff", ctypes.c_float),
                 ("c_coeff", ctypes.c_float), ("live", ctypes.c_int), ("dfe_dfx", vp),
@@ -78,11 +88,16 @@ SIGNATURES = {
                                         ctypes.c_uint64, vp]),
     "mpv_philox_raw": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mpv_convert": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int64, vp]),
+    "mpv_split_workspace_bytes": (ctypes.c_size_t, []),
+    "mpv_split_f16": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(Split16), vp, vp]),
+    "mpv_noise_philox_f16": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.POINTER(Split16), vp]),
     "mpv_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
     "mpv_probit_fwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FwdArgs), vp]),
     "mpv_bstat_combine": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int64, vp, vp]),
     "mpv_probit_finalize": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FinalArgs), vp]),
-    "mpv_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
+    "mpv_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape), ctypes.c_int]),
     "mpv_probit_bwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(BwdArgs), vp]),
     "mpv_kl_bwd": (ctypes.c_int, [ctypes.POINTER(KlBwdArgs), vp]),
     "mpv_reparam_fwd": (ctypes.c_int, [ctypes.POINTER(ReparamArgs), vp]),
@@ -140,7 +155,7 @@ def require_gpu(*tensors):
     load_library()
 
 
-KERNELS = ["noise_philox", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
+KERNELS = ["noise_philox", "split", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
            "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
            "kl_bwd"]
 

@@ -22,17 +22,82 @@ def _f32(t, name):
     return t.contiguous()
 
 
+def _pad(n, m):
+    return (n + m - 1) // m * m
+
+
+class Planes:
+    """3xf16 split operand (include/mpvae_hip.h mpv_split16): value = (hi + lo) / scale,
+    hi/lo fp16 planes of shape (rows_pad, ld), zero padded."""
+
+    def __init__(self, rows_pad, ld, device):
+        self.rows_pad, self.ld = int(rows_pad), int(ld)
+        self.hi = torch.empty((self.rows_pad, self.ld), dtype=torch.int16, device=device)
+        self.lo = torch.empty_like(self.hi)
+        self.scale = torch.empty((1,), dtype=torch.float32, device=device)
+
+    def c(self):
+        return H.Split16(self.hi.data_ptr(), self.lo.data_ptr(), self.scale.data_ptr(),
+                         self.rows_pad, self.ld)
+
+    def value(self):
+        """fp32 value of the planes (tests / diagnostics)."""
+        return (self.hi.view(torch.float16).float() + self.lo.view(torch.float16).float()) \
+            / self.scale
+
+
+GEMMS = {"f16x3": H.GEMM_F16X3, "f32": H.GEMM_F32}
+
+
 class HipShardBackend:
-    """Per-shard arithmetic on the GPU through the C ABI."""
+    """Per-shard arithmetic on the GPU through the C ABI.
+
+    gemm="f16x3" (default): the two noise GEMMs run on the f16 matrix cores
+    with 3xf16 split operands (~fp32 accuracy); gemm="f32": exact fp32 MFMA."""
+
+    def __init__(self, gemm="f16x3"):
+        if gemm not in GEMMS:
+            raise ValueError(f"gemm must be one of {sorted(GEMMS)} (got {gemm!r})")
+        self.gemm = GEMMS[gemm]
 
     def shape(self, S_local, S_total, s_offset, B, L, z):
         return H.Shape(S_local, S_total, s_offset, B, L, z)
 
     def make_noise(self, shape, device, seed, offset):
+        lib, st = H.load_library(), H.stream_of(device)
+        if self.gemm == H.GEMM_F16X3:
+            eps = Planes(shape.S_local * shape.B, _pad(shape.z, 128), device)
+            H.check(lib.mpv_noise_philox_f16(shape, seed, offset, eps.c(), st),
+                    "mpv_noise_philox_f16")
+            return eps
         eps = torch.empty((shape.S_local, shape.B, shape.z), device=device, dtype=torch.float32)
-        H.check(H.load_library().mpv_noise_philox(H.ptr(eps), shape, seed, offset,
-                                                  H.stream_of(device)), "mpv_noise_philox")
+        H.check(lib.mpv_noise_philox(H.ptr(eps), shape, seed, offset, st), "mpv_noise_philox")
         return eps
+
+    def _split(self, x, rows, cols, planes):
+        lib = H.load_library()
+        ws = torch.empty((lib.mpv_split_workspace_bytes(),), device=x.device, dtype=torch.uint8)
+        dt = H.F64 if x.dtype == torch.float64 else H.F32
+        H.check(lib.mpv_split_f16(H.ptr(x), dt, rows, cols, planes.c(), H.ptr(ws),
+                                  H.stream_of(x.device)), "mpv_split_f16")
+        return planes
+
+    def prepare_noise(self, eps, shape):
+        """Explicit (S_local,B,z) fp32 noise -> the GEMM operand."""
+        if self.gemm == H.GEMM_F32:
+            return eps
+        rows = shape.S_local * shape.B
+        return self._split(eps, rows, shape.z, Planes(rows, _pad(shape.z, 128), eps.device))
+
+    def prepare_R(self, R):
+        """r_sqrt_sigma (L,z) fp64/fp32 -> the GEMM operand (R.T.float(), mpvae.py:165)."""
+        if R.dtype not in (torch.float32, torch.float64):
+            raise TypeError(f"r_sqrt_sigma must be float32 or float64 (got {R.dtype})")
+        if self.gemm == H.GEMM_F32:
+            return self.to_f32(R)
+        L, z = R.shape
+        return self._split(R.detach().contiguous(), L, z,
+                           Planes(_pad(L, 128), _pad(z, 128), R.device))
 
     def to_f32(self, R):
         if R.dtype == torch.float32:
@@ -53,7 +118,7 @@ class HipShardBackend:
                                              H.stream_of(x32.device)), "mpv_convert")
         return out
 
-    def forward_local(self, shape, y, fe_out, fx_out, R32, eps, keep_T):
+    def forward_local(self, shape, y, fe_out, fx_out, Rop, eps, keep_T):
         lib = H.load_library()
         dev = y.device
         S, B, L = shape.S_local, shape.B, shape.L
@@ -63,7 +128,11 @@ class HipShardBackend:
         colsum = torch.empty((2, B, L), device=dev, dtype=torch.float32)
         nbytes = lib.mpv_fwd_workspace_bytes(shape)
         ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
-        args = H.FwdArgs(H.ptr(y), H.ptr(fe_out), H.ptr(fx_out), H.ptr(R32), H.ptr(eps), H.ptr(T),
+        if self.gemm == H.GEMM_F16X3:
+            ops = (None, None, Rop.c(), eps.c())
+        else:
+            ops = (H.ptr(Rop), H.ptr(eps), H.Split16(), H.Split16())
+        args = H.FwdArgs(H.ptr(y), H.ptr(fe_out), H.ptr(fx_out), self.gemm, *ops, H.ptr(T),
                          H.ptr(rowstat), H.ptr(bstat), H.ptr(colsum), H.ptr(ws), nbytes)
         H.check(lib.mpv_probit_fwd(shape, args, H.stream_of(dev)), "mpv_probit_fwd")
         return dict(rowstat=rowstat, bstat=bstat, colsum=colsum, T=T)
@@ -98,10 +167,12 @@ class HipShardBackend:
         flat = torch.empty((n_fe + (L * z if want_dR else 0),), device=dev, dtype=torch.float32)
         dfe_dfx = flat[:n_fe].view(2, B, L)
         dR32 = flat[n_fe:].view(L, z) if want_dR else None
-        nbytes = lib.mpv_bwd_workspace_bytes(shape)
+        nbytes = lib.mpv_bwd_workspace_bytes(shape, self.gemm)
         ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
+        eps = saved["eps"]
+        eps_ops = (None, eps.c()) if self.gemm == H.GEMM_F16X3 else (H.ptr(eps), H.Split16())
         args = H.BwdArgs(H.ptr(saved["y"]), H.ptr(saved["fe_out"]), H.ptr(saved["fx_out"]),
-                         H.ptr(saved["eps"]), H.ptr(saved["T"]), H.ptr(saved["rowstat"]),
+                         self.gemm, *eps_ops, H.ptr(saved["T"]), H.ptr(saved["rowstat"]),
                          H.ptr(saved["bstat"]), H.ptr(gscal), H.ptr(g_I), H.ptr(g_IL),
                          nll_coeff, c_coeff, live, H.ptr(dfe_dfx), H.ptr(dR32), H.ptr(ws), nbytes)
         H.check(lib.mpv_probit_bwd(shape, args, H.stream_of(dev)), "mpv_probit_bwd")
@@ -131,11 +202,11 @@ class ElboConfig:
     """Non-tensor arguments of ProbitELBO."""
 
     def __init__(self, S_total, S_local, s_offset, nll_coeff, c_coeff, noise="explicit",
-                 seed=0, offset=0, backend=None, exchange=None):
+                 seed=0, offset=0, backend=None, exchange=None, gemm="f16x3"):
         self.S_total, self.S_local, self.s_offset = int(S_total), int(S_local), int(s_offset)
         self.nll_coeff, self.c_coeff = float(nll_coeff), float(c_coeff)
         self.noise, self.seed, self.offset = noise, int(seed), int(offset)
-        self.backend = backend if backend is not None else HipShardBackend()
+        self.backend = backend if backend is not None else HipShardBackend(gemm)
         self.exchange = exchange if exchange is not None else LocalExchange()
 
 
@@ -162,10 +233,11 @@ class ProbitELBO(torch.autograd.Function):
             eps = _f32(eps, "noise")
             if tuple(eps.shape) != (cfg.S_local, B, z):
                 raise ValueError(f"noise must be {(cfg.S_local, B, z)}, got {tuple(eps.shape)}")
-        R32 = be.to_f32(R)
+            eps = be.prepare_noise(eps, shape)
+        Rop = be.prepare_R(R)
         need = ctx.needs_input_grad
         keep_T = need[1] or need[4] or need[7]
-        loc = be.forward_local(shape, y, fe_out, fx_out, R32, eps, keep_T)
+        loc = be.forward_local(shape, y, fe_out, fx_out, Rop, eps, keep_T)
         bstat, colsum = cfg.exchange.combine(loc["bstat"], loc["colsum"], be)
         outs = be.finalize(shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
                            cfg.nll_coeff, cfg.c_coeff)

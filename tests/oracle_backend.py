@@ -29,8 +29,11 @@ class OracleShardBackend:
         return _t(philox.normal_noise(shape.S_local, shape.B, shape.z, seed, offset,
                                       shape.s_offset))
 
-    def to_f32(self, R):
+    def prepare_R(self, R):
         return R.detach().float().contiguous()
+
+    def prepare_noise(self, eps, shape):
+        return eps
 
     def from_f32(self, x32, dtype):
         return x32.to(dtype)

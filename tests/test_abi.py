@@ -37,8 +37,11 @@ def test_abi_version_and_host_entry_points():
     lib = H.load_library()
     assert lib.mpv_abi_version() == H.ABI_VERSION
     s = H.Shape(4096, 4096, 0, 512, 1024, 1024)
-    fw, bw = lib.mpv_fwd_workspace_bytes(s), lib.mpv_bwd_workspace_bytes(s)
+    fw, bw = lib.mpv_fwd_workspace_bytes(s), lib.mpv_bwd_workspace_bytes(s, H.GEMM_F32)
     assert 0 < fw < 1 << 30 and 0 < bw < 1 << 30
+    # 3xf16: + the two fp16 planes of G (2 x 2 B x B*S x L)
+    bw16 = lib.mpv_bwd_workspace_bytes(s, H.GEMM_F16X3)
+    assert bw16 - bw >= 4 * 512 * 4096 * 1024
     # invalid shapes are rejected on the host, before any launch
     bad = H.Shape(0, 10, 0, 4, 8, 8)
     assert lib.mpv_fwd_workspace_bytes(bad) == 0

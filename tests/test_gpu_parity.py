@@ -93,11 +93,32 @@ def test_philox_kernel_known_answers():
 
 @pytest.mark.parametrize("S,B,z,s_off", [(7, 5, 13, 0), (9, 3, 38, 5), (64, 16, 128, 100)])
 def test_philox_noise_matches_oracle(S, B, z, s_off):
-    be = HipShardBackend()
     shape = H.Shape(S, s_off + S, s_off, B, 4, z)
-    eps = be.make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
     ref = philox.normal_noise(S, B, z, seed=0x1234ABCD5678, s_offset=s_off)
+    eps = HipShardBackend("f32").make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
     np.testing.assert_allclose(_np(eps), ref, atol=2e-5, rtol=2e-5)
+    # the 3xf16 planes hold the same numbers (to the split's 2^-22) and zero padding
+    pl = HipShardBackend("f16x3").make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
+    v = _np(pl.value())
+    assert v.shape == (S * B, pl.ld) and pl.ld % 128 == 0
+    np.testing.assert_allclose(v[:, :z].reshape(S, B, z), ref, atol=2e-5, rtol=2e-5)
+    assert not v[:, z:].any()
+
+
+def test_split_planes_round_trip():
+    """mpv_split_f16: power-of-two scale from max|x|, hi+lo == x to ~2^-22."""
+    be = HipShardBackend("f16x3")
+    g = torch.Generator(device=DEV).manual_seed(9)
+    for scale in (1e-6, 0.05, 3.0, 2e4):
+        R = torch.randn((37, 53), device=DEV, dtype=torch.float64, generator=g) * scale
+        pl = be.prepare_R(R)
+        assert pl.rows_pad == 128 and pl.ld == 128
+        v = pl.value().double()
+        err = (v[:37, :53] - R).abs().max() / R.abs().max()
+        assert float(err) < 1e-6, (scale, float(err))
+        assert float(v[37:].abs().max()) == 0.0 and float(v[:, 53:].abs().max()) == 0.0
+        s = float(pl.scale)
+        assert 2 ** 13 <= float(R.abs().max()) * s < 2 ** 14
 
 
 RANDOM_CASES = [
@@ -111,8 +132,9 @@ RANDOM_CASES = [
 ]
 
 
+@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
 @pytest.mark.parametrize("L,z,B,S,d", RANDOM_CASES)
-def test_random_against_oracle(L, z, B, S, d):
+def test_random_against_oracle(L, z, B, S, d, gemm):
     rng = np.random.default_rng(L * 7 + S)
     y = (rng.random((B, L)) < 0.25).astype(np.float32)
     y[:, 0], y[:, 1] = 1, 0
@@ -133,7 +155,7 @@ def test_random_against_oracle(L, z, B, S, d):
         t[k].requires_grad_(True)
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
                               mode="train", nll_coeff=0.5, c_coeff=10.0,
-                              mpvae_noise=torch.from_numpy(noise))
+                              mpvae_noise=torch.from_numpy(noise), mpvae_gemm=gemm)
     out = _call(t, args)
     for k, o in zip(OUTS, out):
         assert rel_err(_np(o), ref[k]) <= FWD_RTOL, (k, rel_err(_np(o), ref[k]))
@@ -159,13 +181,13 @@ def test_shard_invariance_at_c4_size():
     R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
          * (6.0 / (L + z)) ** 0.5)
     be = HipShardBackend()
-    R32 = be.to_f32(R)
+    Rop = be.prepare_R(R)
     seed = 987654321
 
     def local(S_loc, s_off):
         shape = be.shape(S_loc, S, s_off, B, L, z)
         eps = be.make_noise(shape, DEV, seed, 0)
-        return shape, be.forward_local(shape, y, fe, fx, R32, eps, keep_T=False)
+        return shape, be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=False)
 
     shape, full = local(S, 0)
     out_full = be.finalize(shape, full["bstat"], full["colsum"], *mus, 0.5, 10.0)
@@ -204,6 +226,33 @@ def test_full_size_train_step_is_finite_and_deterministic():
     for a, b in zip(*res):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+def test_gemm_modes_agree_at_c4_dims():
+    """3xf16 split GEMMs vs exact fp32 MFMA on the same philox noise, at the
+    headline L=z=1024, n_sample=4096 (batch 64 to keep the test short)."""
+    B, S, L, z, d = 64, 4096, 1024, 1024, 50
+    g = torch.Generator(device=DEV).manual_seed(21)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    base = [torch.randn((B, L), device=DEV, generator=g) for _ in range(2)]
+    mus = [torch.randn((B, d), device=DEV, generator=g) * s for s in (1, 0.1, 1, 0.1)]
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.054
+    res = {}
+    for gemm in ("f16x3", "f32"):
+        args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
+                                  mode="train", nll_coeff=0.1, c_coeff=200.0,
+                                  mpvae_noise="philox", mpvae_seed=7, mpvae_gemm=gemm)
+        leaves = [x.clone().requires_grad_(True) for x in [base[0], mus[0], mus[1], base[1],
+                                                            mus[2], mus[3], R]]
+        out = mpvae.compute_loss(y, *leaves, args)
+        (out[0] + out[6].sum()).backward()
+        res[gemm] = [_np(o) for o in out] + [_np(x.grad) for x in leaves]
+    names = OUTS + ["d" + k for k in ["fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu",
+                                       "fx_logvar", "r_sqrt_sigma"]]
+    for k, a, b in zip(names, res["f16x3"], res["f32"]):
+        tol = FWD_RTOL if not k.startswith("d") else 2e-4
+        assert rel_err(a, b) <= tol, (k, rel_err(a, b))
 
 
 def test_test_mode_forward_only_large_s():
