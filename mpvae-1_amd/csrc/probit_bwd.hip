@@ -106,16 +106,18 @@ struct ElemParams {
 MPV_DEV float d_elem(float t, float base, float y, bool soft, float alpha, float bP, float bN,
                      float gind) {
   const float u = t + base;
-  const float E = probit_prob(u);
+  float phi;
+  const float E = probit_eval(u, phi);
   // d logp / dE = y/E - (1-y)/(1-E)  (mpvae.py:184-185)
-  float dl = (y == 0.0f) ? -1.0f / (1.0f - E) : 1.0f / E;
+  float dl = (y == 0.0f) ? -fast_rcp(1.0f - E) : fast_rcp(E);
   if (soft) dl = y / E - (1.0f - y) / (1.0f - E);
   float dE = alpha * dl + gind;
-  if (y == 1.0f) dE -= bP * expf(-5.0f * E);
-  if (y == 0.0f) dE += bN * expf(5.0f * E);
+  // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
+  const float rk = (y == 1.0f) ? -bP : ((y == 0.0f) ? bN : 0.0f);
+  dE = fmaf(rk, fast_exp((y == 1.0f ? -5.0f : 5.0f) * E), dE);
   // a degenerate row poisons every label, whatever its value (reference autograd)
   if (bP != bP) dE = bP;
-  return dE * kC1 * kInvSqrt2Pi * expf(-0.5f * u * u);
+  return dE * kC1 * phi;
 }
 
 template <bool VEC, bool PLANES>

@@ -117,15 +117,15 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
         const float Ex = probit_prob(t + ln.fx[n]);
         const float y = ln.y[n];
         // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
-        float le = logf(y == 0.0f ? 1.0f - E : E);
-        float lx = logf(y == 0.0f ? 1.0f - Ex : Ex);
+        float le = fast_log(y == 0.0f ? 1.0f - E : E);
+        float lx = fast_log(y == 0.0f ? 1.0f - Ex : Ex);
         if (ln.soft[n]) {
-          le = y * logf(E) + (1.0f - y) * logf(1.0f - E);
-          lx = y * logf(Ex) + (1.0f - y) * logf(1.0f - Ex);
+          le = y * fast_log(E) + (1.0f - y) * fast_log(1.0f - E);
+          lx = y * fast_log(Ex) + (1.0f - y) * fast_log(1.0f - Ex);
         }
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
         const float sg = (y == 1.0f) ? -5.0f : 5.0f;
-        const float re = expf(sg * E), rx = expf(sg * Ex);
+        const float re = fast_exp(sg * E), rx = fast_exp(sg * Ex);
         const float wpos = (ok && y == 1.0f) ? 1.0f : 0.0f;
         const float wneg = (ok && y == 0.0f) ? 1.0f : 0.0f;
         st6[0] += ok ? le : 0.0f;
@@ -614,7 +614,9 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 2>), grid, dim3(512), 0, st, p);
         break;
       default:  // BN 128, 8 waves, double-buffered (128 KB)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<2, 4, 4, 2, 2>), grid, dim3(512), 0, st, p);
+        // waves 4 (rows) x 2 (labels): 4 label columns per lane halve the
+        // DPP row-reduction cost per element against a 2 x 4 layout
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 4, 2>), grid, dim3(512), 0, st, p);
         break;
     }
   }
