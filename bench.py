@@ -30,6 +30,12 @@ import mpvae_hip as H  # noqa: E402
 
 METRIC = "probit MC label-samples/sec (B×n_sample×L) at 1/2/4/8 GPU; ELBO rel-err"
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
+F16_MFMA_PEAK = 2.5e15      # MI355X_MICROARCH.md: dense BF16/F16 MFMA
+# The f16x3 GEMMs evaluate one fp32-accurate multiply-add as three f16 MFMA
+# products (hi*hi + hi*lo + lo*hi), so their fp32-equivalent ceiling is a third
+# of the dense f16 peak.
+PEAKS = {"f16x3": (F16_MFMA_PEAK / 3.0, "f16x3 MFMA: dense f16 peak / 3"),
+         "f32": (FP32_MFMA_PEAK, "f32 MFMA")}
 HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec
 
 # name: (L, z, B, n_sample per GPU (weak) or total (strong), d, nll_coeff, c_coeff, scaling)
@@ -86,11 +92,13 @@ def step(y, leaves, args, it):
     return out
 
 
-def roofline(times, S_local, B, L, z, steps):
-    """Dominant kernel's achieved rate vs its bound, from in-library HIP events."""
+def roofline(times, S_local, B, L, z, steps, gemm):
+    """Dominant kernel's achieved rate vs its bound, from in-library HIP events.
+    GEMM work is the algorithmic fp32 GEMM (2*S*B*L*z flops per launch)."""
+    mfma_peak, peak_note = PEAKS[gemm]
     work = {  # algorithmic work per launch
-        "probit_fwd": ("mfma", 2.0 * S_local * B * L * z, FP32_MFMA_PEAK, "TFLOP/s"),
-        "dR_gemm": ("mfma", 2.0 * S_local * B * L * z, FP32_MFMA_PEAK, "TFLOP/s"),
+        "probit_fwd": ("mfma", 2.0 * S_local * B * L * z, mfma_peak, "TFLOP/s"),
+        "dR_gemm": ("mfma", 2.0 * S_local * B * L * z, mfma_peak, "TFLOP/s"),
         "bwd_elem": ("hbm", 8.0 * S_local * B * L, HBM_PEAK, "GB/s"),
         "noise_philox": ("hbm", 4.0 * S_local * B * z, HBM_PEAK, "GB/s"),
     }
@@ -108,7 +116,8 @@ def roofline(times, S_local, B, L, z, steps):
     breakdown = {k: round(v[1] / v[0], 4) for k, v in sorted(times.items(),
                                                                  key=lambda kv: -kv[1][1])}
     return {"kernel": dom, "bound": bound, "achieved": achieved, "peak": pk, "unit": unit,
-            "frac": frac, "traffic": None, "avg_ms": round(avg_s * 1e3, 4),
+            "frac": frac, "traffic": None, "peak_basis": peak_note if bound == "mfma" else
+            "HBM3E spec", "avg_ms": round(avg_s * 1e3, 4),
             "per_launch_ms": breakdown}
 
 
@@ -178,6 +187,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=int, default=2)
     ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--gemm", default="f16x3", choices=sorted(PEAKS))
     cli = ap.parse_args()
 
     world, rank, local = setup_dist()
@@ -189,7 +199,8 @@ def main():
     S_local = S if scaling == "weak" else S // world
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_total,
                               n_test_sample=S_total, mode="train", nll_coeff=nllc, c_coeff=cc,
-                              mpvae_noise="philox", mpvae_shard=world > 1)
+                              mpvae_noise="philox", mpvae_shard=world > 1,
+                              mpvae_gemm=cli.gemm)
     y, leaves = make_inputs(L, z, B, d, device)
     lib = H.load_library()
 
@@ -216,7 +227,7 @@ def main():
         elapsed = float(t)
     finite = bool(torch.isfinite(out[0]).item())
     value = S_total * B * L * cli.steps / elapsed
-    rl = roofline(times, S_local, B, L, z, cli.steps)
+    rl = roofline(times, S_local, B, L, z, cli.steps, cli.gemm)
     rl["traffic"], rl["traffic_source"] = pmc_traffic(cli.config, rl["kernel"])
 
     cpu, errs = None, None
@@ -233,7 +244,7 @@ def main():
             "config": {"workload": f"{cli.config}: compute_loss fwd+bwd, B={B}, L={L}, z={z}, "
                                    f"n_sample={S_total} ({S_local}/GPU), philox noise on device",
                        "global_batch": B, "n_sample": S_total, "label_dim": L, "z_dim": z,
-                       "parallelism": f"n_sample-sharded x{world}"},
+                       "parallelism": f"n_sample-sharded x{world}", "gemm": cli.gemm},
             "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
         }
         print(json.dumps(line), flush=True)

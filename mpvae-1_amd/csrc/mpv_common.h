@@ -140,6 +140,38 @@ MPV_DEV float pow2_scale(float maxabs) {
 
 MPV_DEV f16x8 as_f16x8(s16x8 v) { return __builtin_bit_cast(f16x8, v); }
 
+// ---- LDS-DMA pipelines: raw barrier + counted vmcnt ------------------------
+// __syncthreads() would make hipcc drain every in-flight LDS-DMA (vmcnt(0));
+// the rings use a raw s_barrier and wait for exactly the stages they read.
+MPV_DEV void barrier_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+MPV_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (the immediate must be a constant).
+MPV_DEV void wait_vmcnt_dyn(int n) {
+#define MPV_VMC(k) \
+  case k:          \
+    wait_vmcnt<k>(); \
+    break;
+  switch (n) {
+    MPV_VMC(0) MPV_VMC(1) MPV_VMC(2) MPV_VMC(3) MPV_VMC(4) MPV_VMC(5) MPV_VMC(6) MPV_VMC(7)
+    MPV_VMC(8) MPV_VMC(9) MPV_VMC(10) MPV_VMC(11) MPV_VMC(12) MPV_VMC(13) MPV_VMC(14)
+    MPV_VMC(15) MPV_VMC(16) MPV_VMC(17) MPV_VMC(18) MPV_VMC(19) MPV_VMC(20) MPV_VMC(21)
+    MPV_VMC(22) MPV_VMC(23) MPV_VMC(24)
+    default:
+      wait_vmcnt<0>();
+      break;
+  }
+#undef MPV_VMC
+}
+
 // ---- Philox4x32-10 (Salmon et al. SC'11) ------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
         uint16_t h[4], l[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
-        const int64_t o = cb * p.ldg + c0;  // ldg % 4 == 0 and c0 + 3 < ldg
+        const int64_t o = ((int64_t)s * B + b) * p.ldg + c0;  // s-major rows; ldg % 4 == 0
         *reinterpret_cast<s16x4*>(p.g_hi + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
         *reinterpret_cast<s16x4*>(p.g_lo + o) = s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
       } else if (VEC && c0 + 3 < L) {
@@ -211,19 +211,22 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
 }
 
 // ------------------------------------------------------------ 3xf16 dR GEMM
-// LDS image per stage: [G_hi | G_lo | E_hi | E_lo], each 64 rows (the K axis:
-// rows q = b*S + s of this chunk) x 128 columns x 2 B = 256 B per row.  The
-// 32-B chunk c of row r sits at position c ^ (r & 7).  An MFMA fragment
-// (8 consecutive K rows of one column per lane) is two ds_read_b64_tr_b16;
-// within each K step the 32 rows are permuted so that a 32-lane half of one
-// transposed read touches rows 8j..8j+7 -> 8 distinct 32-B chunk positions,
-// all 64 banks once: conflict-free.  Element j of lane group g holds K row
-// 32*ks + (j < 4 ? 4g + j : 16 + 4g + j - 4), the same for A and B.
+// K axis = the S*B sample rows r = s*B + b: the noise planes' own row order, in
+// which the element pass also writes the G planes, so a K row is one address
+// for both operands.  The rows stream in stages of 32 through a 4-deep ring of
+// LDS buffers (LDS-DMA, 3 stages in flight, one barrier per stage).  Stage
+// image: [G_hi | G_lo | E_hi | E_lo], 32 rows x 128 columns x 2 B = 256 B per
+// row; the 32-B chunk c of row r sits at position c ^ (r & 7).  An MFMA
+// fragment (8 K rows of one column per lane) is two ds_read_b64_tr_b16; lane
+// group g reads rows 4g..4g+3 and 16+4g..16+4g+3, so a 32-lane half of one
+// transposed read touches rows 8j..8j+7 -> 8 distinct 32-B positions, all 64
+// banks once: conflict-free.  Element j of lane group g holds K row
+// (j < 4 ? 4g + j : 16 + 4g + j - 4), the same for A and B.
 struct Dr16Params {
   const uint16_t* g_hi;
   const uint16_t* g_lo;
   const float* g_scale;
-  int64_t ldg;          // G plane row length (>= nLt*128)
+  int64_t ldg;          // G plane row length (>= nLt*128), rows s*B + b
   mpv_split16 eps16;    // rows s*B + b, ld >= nZt*128
   float* slab;          // [nKc][L][z]
   int S, B, L, z;
@@ -231,18 +234,7 @@ struct Dr16Params {
 };
 
 constexpr int kDrRowB = 256;  // bytes per LDS row (128 halves)
-constexpr int kDrKR = 64;     // K rows per chunk
-
-MPV_DEV void barrier_raw() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int N>
-MPV_DEV void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -263,17 +255,38 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
   }
 }
 
-template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(WM* WN * 64) void dR16_kernel(Dr16Params p) {
+// One stage's LDS-DMA for this wave: PER_WAVE 1-KB groups of 4 rows each,
+// written from `dst` on (wave-uniform).
+template <int PER_WAVE>
+MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, const int (&dma_r)[PER_WAVE],
+                      const int (&dma_off)[PER_WAVE], const int (&dma_plane)[PER_WAVE]) {
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int q = q0 + dma_r[i];
+    const uint16_t* src;
+    if (dma_plane[i] < 2) {
+      src = (dma_plane[i] ? p.g_lo : p.g_hi) + (int64_t)q * p.ldg;  // G rows >= rows are zero
+    } else {
+      src = (dma_plane[i] == 3 ? p.eps16.lo : p.eps16.hi) + (int64_t)min(q, rows - 1) * p.eps16.ld;
+    }
+    __builtin_amdgcn_global_load_lds(src + dma_off[i],
+                                     (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
+                                     0, 0);
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int kDrStages>
+__global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
   constexpr int NW = WM * WN;
   constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
   static_assert(BL == 128 && BZ == 128, "tile is 128 x 128 (one 256-B LDS row)");
-  constexpr int PLANE = kDrKR * kDrRowB;  // 16 KB
-  constexpr int STAGE = 4 * PLANE;
-  constexpr int GROUPS = STAGE / 1024;    // 64 wave-instructions (4 rows each)
+  constexpr int PLANE = kDrKR * kDrRowB;  // 8 KB
+  constexpr int STAGE = 4 * PLANE;        // 32 KB
+  constexpr int GROUPS = STAGE / 1024;    // 32 wave-instructions of 4 rows
   static_assert(GROUPS % NW == 0, "DMA groups must split over waves");
   constexpr int PER_WAVE = GROUPS / NW;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  constexpr int P = kDrStages - 1;
+  __shared__ __attribute__((aligned(1024))) char smem[kDrStages * STAGE];
 
   int kc, tile;
   decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
@@ -282,14 +295,24 @@ __global__ __launch_bounds__(WM* WN * 64) void dR16_kernel(Dr16Params p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.S, B = p.B, rows = B * S;
+  const int rows = p.B * p.S;
   const int q_begin = kc * p.rows_per_chunk;
   const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
-  const int64_t lde = p.eps16.ld;
-  // DMA lane mapping: 4 rows of 256 B per 1-KB wave-instruction
+  // DMA lane mapping: 4 rows of 256 B per 1-KB wave-instruction; per-lane
+  // element offsets (without the stage's first row) of my PER_WAVE groups
   const int dma_row = lane >> 4, dma_c = (lane & 15) >> 1, dma_half = lane & 1;
+  int dma_r[PER_WAVE], dma_off[PER_WAVE], dma_plane[PER_WAVE];
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int grp = wid * PER_WAVE + i;
+    dma_plane[i] = grp >> 3;                    // 8 groups (32 rows) per plane
+    dma_r[i] = ((grp & 7) << 2) + dma_row;      // K row within the stage
+    const int col = ((dma_c ^ (dma_r[i] & 7)) << 4) + dma_half * 8;
+    dma_off[i] = (dma_plane[i] < 2 ? l0 : z0) + col;
+  }
   // transposed-read lane mapping: lane 4q+p of its 16-lane group
   const int tq = lr >> 2, tp = lr & 3;
+  const int r0 = lg * 4 + tq, r1 = r0 + 16, sw = r0 & 7;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -297,80 +320,50 @@ __global__ __launch_bounds__(WM* WN * 64) void dR16_kernel(Dr16Params p) {
 #pragma unroll
     for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto issue = [&](int stage, int q0) {
-#pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i) {
-      const int grp = wid * PER_WAVE + i;
-      const int plane = grp >> 4;                 // 16 groups (64 rows) per plane
-      const int r = ((grp & 15) << 2) + dma_row;  // K row within the chunk
-      const int c = dma_c ^ (r & 7);              // source 32-B chunk for this LDS slot
-      const int q = q0 + r;
-      const uint16_t* src;
-      if (plane < 2) {
-        src = (plane ? p.g_lo : p.g_hi) + (int64_t)q * p.ldg + l0;
-      } else {
-        const int qq = min(q, rows - 1);          // G rows >= rows are zero
-        const int bb = qq / S, s = qq - bb * S;
-        src = (plane == 3 ? p.eps16.lo : p.eps16.hi) + ((int64_t)s * B + bb) * lde + z0;
-      }
-      src += c * 16 + dma_half * 8;
-      __builtin_amdgcn_global_load_lds(
-          src, (__attribute__((address_space(3))) void*)(smem + stage * STAGE + grp * 1024), 16, 0,
-          0);
-    }
-  };
 
-  const int nchunk = (q_end - q_begin + kDrKR - 1) / kDrKR;
-  if (nchunk > 0) issue(0, q_begin);
-  for (int ci = 0; ci < nchunk; ++ci) {
-    const int cur = ci & 1;
-    if (ci + 1 < nchunk) {
-      issue(cur ^ 1, q_begin + (ci + 1) * kDrKR);
-      wait_vmcnt<PER_WAVE>();
-    } else {
-      wait_vmcnt<0>();
+  const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
+  for (int j = 0; j < P && j < nst; ++j)
+    dr_issue<PER_WAVE>(p, smem + j * STAGE + wid * PER_WAVE * 1024, q_begin + j * kDrKR, rows,
+                       dma_r, dma_off, dma_plane);
+  for (int ci = 0; ci < nst; ++ci) {
+    wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
+    if (ci + P < nst)
+      dr_issue<PER_WAVE>(p, smem + ((ci + P) % kDrStages) * STAGE + wid * PER_WAVE * 1024,
+                         q_begin + (ci + P) * kDrKR, rows, dma_r, dma_off, dma_plane);
+    const char* base = smem + (ci % kDrStages) * STAGE;
+    s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      const int cofs = (((wm * TM + m) ^ sw) << 5) + tp * 8;
+      ah[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + cofs),
+                                      tr_read(base, r1 * kDrRowB + cofs), 0, 1, 2, 3, 4, 5, 6, 7);
+      al[m] = __builtin_shufflevector(tr_read(base + PLANE, r0 * kDrRowB + cofs),
+                                      tr_read(base + PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3, 4,
+                                      5, 6, 7);
     }
-    barrier_raw();
-    const char* base = smem + cur * STAGE;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      s16x8 ah[TM], al[TM], bh[TN], bl[TN];
-      const int r0 = ks * 32 + lg * 4 + tq, r1 = r0 + 16;
-      const int sw = r0 & 7;  // == r1 & 7
+    for (int n = 0; n < TN; ++n) {
+      const int cofs = (((wn * TN + n) ^ sw) << 5) + tp * 8;
+      bh[n] = __builtin_shufflevector(tr_read(base + 2 * PLANE, r0 * kDrRowB + cofs),
+                                      tr_read(base + 2 * PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3,
+                                      4, 5, 6, 7);
+      bl[n] = __builtin_shufflevector(tr_read(base + 3 * PLANE, r0 * kDrRowB + cofs),
+                                      tr_read(base + 3 * PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3,
+                                      4, 5, 6, 7);
+    }
 #pragma unroll
-      for (int m = 0; m < TM; ++m) {
-        const int cofs = (((wm * TM + m) ^ sw) << 5) + tp * 8;
-        const s16x4 h0 = tr_read(base, r0 * kDrRowB + cofs);
-        const s16x4 h1 = tr_read(base, r1 * kDrRowB + cofs);
-        const s16x4 l0v = tr_read(base + PLANE, r0 * kDrRowB + cofs);
-        const s16x4 l1v = tr_read(base + PLANE, r1 * kDrRowB + cofs);
-        ah[m] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-        al[m] = __builtin_shufflevector(l0v, l1v, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
+    for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
-        const int cofs = (((wn * TN + n) ^ sw) << 5) + tp * 8;
-        const s16x4 h0 = tr_read(base + 2 * PLANE, r0 * kDrRowB + cofs);
-        const s16x4 h1 = tr_read(base + 2 * PLANE, r1 * kDrRowB + cofs);
-        const s16x4 l0v = tr_read(base + 3 * PLANE, r0 * kDrRowB + cofs);
-        const s16x4 l1v = tr_read(base + 3 * PLANE, r1 * kDrRowB + cofs);
-        bh[n] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-        bl[n] = __builtin_shufflevector(l0v, l1v, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
+                                                           acc[m][n], 0, 0, 0);
       }
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
-                                                             acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
-                                                             acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
-                                                             acc[m][n], 0, 0, 0);
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();
   }
   const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
   // D[i = l][j = z]: row = lg*4 + reg, col = lr
@@ -563,7 +556,7 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.nZt = (int)cdiv(z, 128);
   const int64_t rows = B * S;
   const int64_t tiles = (int64_t)pl.nLt * pl.nZt;
-  const int64_t kr = planes ? 64 : 32;  // K rows per chunk of the GEMM
+  const int64_t kr = 32;  // K rows per stage of either GEMM
   pl.rows_pad = (int)(cdiv(rows, kr) * kr);
   int64_t kc = cdiv(1536, tiles);
   const int64_t kc_max = cdiv(rows, 256);
@@ -695,7 +688,8 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.nKc = pl.nKc;
       dp.rows_per_chunk = pl.dr_rows_per_chunk;
       dp.rows_pad = pl.rows_pad;
-      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+      // 4 waves of 64 x 64, 2-stage ring (64 KB LDS): 2 workgroups per CU
+      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 4, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
     } else {
       DrParams dp;
       dp.G = a->T;

@@ -143,6 +143,7 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
 #pragma unroll
         for (int k = 0; k < 6; ++k) red[(wn * BM + rl) * 6 + k] = st6[k];
       }
+      if (TM * TN > 8) __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one m-slab
   }
@@ -330,34 +331,44 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
 }
 
 // ------------------------------------------------------ 3xf16 mainloop
-// LDS image per stage: [A_hi | A_lo | B_hi | B_lo], each row 128 B = 64 halves
-// of one K chunk.  A 16-B chunk c of row r sits at position c ^ ((r >> 1) & 7):
-// the ds_read_b128 fragment reads (16 rows x one 16-B column per lane group)
-// then hit 16 distinct slots of the 256-B bank row (checked by script, see
-// DESIGN.md).  LDS-DMA writes lane-linearly, so the swizzle is applied to the
-// per-lane SOURCE address and undone by the same XOR on the read.
-constexpr int kRowB = 128;  // bytes per plane row per K chunk (64 halves)
+// The K axis (z) is streamed in stages of 32 halves (one MFMA k-step) through a
+// ring of NSTAGE LDS buffers filled by LDS-DMA (global_load_lds_dwordx4), with
+// NSTAGE-1 stages in flight and one barrier per stage.  Stage image:
+// [A_hi | A_lo | B_hi | B_lo], each row 64 B; the 16-B chunk c of row r sits at
+// position c ^ ((r >> 1) & 3), which makes the ds_read_b128 fragment reads
+// (16 rows x one 16-B column per lane group) hit 16 distinct slots of the
+// 256-B bank row (exhaustively checked).  LDS-DMA writes
+// lane-linearly, so the swizzle goes on the per-lane SOURCE address and the
+// same XOR is applied on the read.
+constexpr int kKC = 32;    // K halves per stage
+constexpr int kRowB = 64;  // bytes per plane row per stage
 
-MPV_DEV void barrier_raw() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int N>
-MPV_DEV void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+// One K stage (k0 halves in) of this wave's DMA groups into stage image `dst`.
+// A device function rather than a lambda: hipcc drops the host stub of a
+// template kernel whose lambda captures arrays.
+template <int GMAX, int GROUPS, int NW>
+MPV_DEV void fwd16_issue(char* dst, int k0, int wid, const char* const (&gbase)[GMAX],
+                         const uint32_t (&goff)[GMAX]) {
+#pragma unroll
+  for (int i = 0; i < GMAX; ++i) {
+    const int grp = wid + i * NW;
+    if (GROUPS % NW != 0 && grp >= GROUPS) break;
+    __builtin_amdgcn_global_load_lds(gbase[i] + 2 * k0 + goff[i],
+                                     (__attribute__((address_space(3))) void*)(dst + grp * 1024),
+                                     16, 0, 0);
+  }
 }
 
 template <int WM, int WN, int TM, int TN, int NSTAGE>
-__global__ __launch_bounds__(WM* WN * 64) void probit_fwd16_kernel(FwdParams p) {
+__global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fwd16_kernel(FwdParams p) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   constexpr int PLANE_A = BM * kRowB, PLANE_B = BN * kRowB;
   constexpr int STAGE = 2 * PLANE_A + 2 * PLANE_B;
-  constexpr int GROUPS = STAGE / 1024;  // 1-KB LDS-DMA wave-instructions per stage
-  static_assert(STAGE % 1024 == 0 && GROUPS % NW == 0, "DMA groups must split over waves");
-  constexpr int PER_WAVE = GROUPS / NW;
+  static_assert(STAGE % 1024 == 0, "stage must be whole 1-KB DMA groups");
+  constexpr int GROUPS = STAGE / 1024;  // 16 rows each
+  constexpr int GMAX = (GROUPS + NW - 1) / NW;
+  constexpr int P = NSTAGE - 1;         // stages in flight
   __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
 
   int g, nt;
@@ -374,38 +385,44 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd16_kernel(FwdParams p) 
   FwdLane<TN> ln;
   fwd_lane_init<WN, TN>(ln, p, b, n0, wn, lr);
   const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
-  const int nK = (p.z + 63) / 64;
-  const int sw_r = (lr >> 1) & 7;        // swizzle of every fragment row this lane reads
-  const int dma_row = lane >> 3;         // row within a 1-KB group
-  const int dma_pos = lane & 7;          // 16-B position within the row
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int coff = (lg ^ ((lr >> 1) & 3)) << 4;  // swizzled 16-B column of this lane's reads
+  const int my_groups = (GROUPS - wid + NW - 1) / NW;
+  const int dma_row = lane >> 2, dma_pos = lane & 3;
 
   const int st_end = min(p.nSt, (sc + 1) * p.tps);
   for (int st = sc * p.tps; st < st_end; ++st) {
     const int s0 = st * BM;
-    // issue one K chunk of all four planes into `stage`
-    auto issue = [&](int stage, int k0) {
+    // DMA sources of this wave's groups (wid, wid+NW, ... of 16 rows; a group
+    // never straddles planes): a wave-uniform 64-bit plane/tile base plus a
+    // 32-bit per-lane byte offset (row within the tile, swizzled chunk), so
+    // the loop carries one VGPR per group and issues the saddr form.
+    const char* gbase[GMAX];
+    uint32_t goff[GMAX];
 #pragma unroll
-      for (int i = 0; i < PER_WAVE; ++i) {
-        const int grp = wid * PER_WAVE + i;
-        const int row = grp * 8 + dma_row;  // row in the concatenated planes
-        const uint16_t* src;
-        int r;
-        if (row < 2 * BM) {
-          const int plane = row >= BM;
-          r = row - plane * BM;
-          const int s = min(s0 + r, S - 1);
-          src = (plane ? p.eps16.lo : p.eps16.hi) + ((int64_t)s * B + b) * lda + k0;
-        } else {
-          const int plane = row >= 2 * BM + BN;
-          r = row - 2 * BM - plane * BN;
-          src = (plane ? p.R16.lo : p.R16.hi) + (int64_t)(n0 + r) * ldb + k0;
-        }
-        src += (dma_pos ^ ((r >> 1) & 7)) * 8;
-        __builtin_amdgcn_global_load_lds(
-            src, (__attribute__((address_space(3))) void*)(smem + stage * STAGE + grp * 1024), 16,
-            0, 0);
+    for (int i = 0; i < GMAX; ++i) {
+      const int grp = min(wid + i * NW, GROUPS - 1);
+      const int row0 = grp * 16;  // wave-uniform first row of the group
+      const int r16 = dma_row;
+      int r;
+      if (row0 < 2 * BM) {
+        const int plane = row0 >= BM;
+        const int rb = row0 - plane * BM;  // uniform
+        r = rb + r16;
+        const int s = min(s0 + r, S - 1);
+        gbase[i] = reinterpret_cast<const char*>((plane ? p.eps16.lo : p.eps16.hi) +
+                                                 ((int64_t)s0 * B + b) * lda);
+        goff[i] = (uint32_t)((int64_t)(s - s0) * B * lda * 2);
+      } else {
+        const int plane = row0 >= 2 * BM + BN;
+        const int rb = row0 - 2 * BM - plane * BN;
+        r = rb + r16;
+        gbase[i] = reinterpret_cast<const char*>((plane ? p.R16.lo : p.R16.hi) +
+                                                 (int64_t)n0 * ldb);
+        goff[i] = (uint32_t)(r * ldb * 2);
       }
-    };
+      goff[i] += (uint32_t)((dma_pos ^ ((r >> 1) & 3)) * 16);
+    }
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -413,48 +430,39 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd16_kernel(FwdParams p) 
 #pragma unroll
       for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    issue(0, 0);
+    for (int j = 0; j < P && j < nK; ++j) fwd16_issue<GMAX, GROUPS, NW>(smem + j * STAGE, j * kKC, wid, gbase, goff);
     for (int kc = 0; kc < nK; ++kc) {
-      const int cur = NSTAGE == 2 ? (kc & 1) : 0;
-      if (NSTAGE == 2 && kc + 1 < nK) {
-        issue(cur ^ 1, (kc + 1) * 64);
-        wait_vmcnt<PER_WAVE>();
-      } else {
-        wait_vmcnt<0>();
+      // stages issued after kc may stay in flight; kc itself must have landed
+      wait_vmcnt_dyn(min(P - 1, nK - 1 - kc) * my_groups);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // kc landed for every wave; every wave is done reading kc-1
+      if (kc + P < nK) fwd16_issue<GMAX, GROUPS, NW>(smem + ((kc + P) % NSTAGE) * STAGE, (kc + P) * kKC, wid,
+                                                gbase, goff);
+      const char* base = smem + (kc % NSTAGE) * STAGE;
+      s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+        const int off = ((wm * TM + m) * 16 + lr) * kRowB + coff;
+        ah[m] = *reinterpret_cast<const s16x8*>(base + off);
+        al[m] = *reinterpret_cast<const s16x8*>(base + PLANE_A + off);
       }
-      barrier_raw();
-      const char* base = smem + cur * STAGE;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int coff = (((4 * ks + lg) ^ sw_r) << 4);
-        s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      for (int n = 0; n < TN; ++n) {
+        const int off = 2 * PLANE_A + ((wn * TN + n) * 16 + lr) * kRowB + coff;
+        bh[n] = *reinterpret_cast<const s16x8*>(base + off);
+        bl[n] = *reinterpret_cast<const s16x8*>(base + PLANE_B + off);
+      }
 #pragma unroll
-        for (int m = 0; m < TM; ++m) {
-          const int off = ((wm * TM + m) * 16 + lr) * kRowB + coff;
-          ah[m] = *reinterpret_cast<const s16x8*>(base + off);
-          al[m] = *reinterpret_cast<const s16x8*>(base + PLANE_A + off);
-        }
+      for (int m = 0; m < TM; ++m)
 #pragma unroll
         for (int n = 0; n < TN; ++n) {
-          const int off = 2 * PLANE_A + ((wn * TN + n) * 16 + lr) * kRowB + coff;
-          bh[n] = *reinterpret_cast<const s16x8*>(base + off);
-          bl[n] = *reinterpret_cast<const s16x8*>(base + PLANE_B + off);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
+                                                             acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
+                                                             acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
+                                                             acc[m][n], 0, 0, 0);
         }
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int n = 0; n < TN; ++n) {
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
-                                                               acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
-                                                               acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
-                                                               acc[m][n], 0, 0, 0);
-          }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier_raw();
-      if (NSTAGE == 1 && kc + 1 < nK) issue(0, (kc + 1) * 64);
     }
     fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, nt,
                                       reinterpret_cast<float*>(smem));
@@ -607,16 +615,16 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
     }
   } else {
     switch (pl.cfg) {
-      case 0:  // BN 48, 4 waves, single-buffered (44 KB LDS: 3 workgroups per CU)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 1>), grid, dim3(256), 0, st, p);
+      case 0:  // BN 48, 4 waves, 3-stage ring (66 KB LDS: 2 workgroups per CU)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 3>), grid, dim3(256), 0, st, p);
         break;
-      case 1:  // BN 96, 8 waves, double-buffered (112 KB)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 2>), grid, dim3(512), 0, st, p);
+      case 1:  // BN 96, 8 waves, 4-stage ring (112 KB)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
         break;
-      default:  // BN 128, 8 waves, double-buffered (128 KB)
-        // waves 4 (rows) x 2 (labels): 4 label columns per lane halve the
-        // DPP row-reduction cost per element against a 2 x 4 layout
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 4, 2>), grid, dim3(512), 0, st, p);
+      default:  // 128 x 128 tile, 4 waves of 64 x 64 (3 MFMAs per 1.33 fragment
+                // reads), 2-stage ring (64 KB): 2 workgroups per CU, so one
+                // workgroup's epilogue (VALU) overlaps the other's MFMA phase
+        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
         break;
     }
   }
@@ -659,6 +667,10 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
     const int64_t zp = cdiv(shape->z, 64) * 64;
     if (int rc = check_split_operand(a->R16, (int64_t)pl.nNt * pl.BN, zp, "R16")) return rc;
     if (int rc = check_split_operand(a->eps16, shape->S_local * shape->B, zp, "eps16")) return rc;
+    // the DMA issue keeps per-lane byte offsets within one s/l tile in 32 bits
+    MPV_REQUIRE((int64_t)pl.BM * shape->B * a->eps16.ld * 2 < (int64_t(1) << 32) &&
+                    (int64_t)pl.BN * a->R16.ld * 2 < (int64_t(1) << 32),
+                "B * ld too large for the f16x3 tile offsets");
   }
   MPV_REQUIRE(a->workspace_bytes >= pl.rowpart_bytes + pl.colpart_bytes,
               "workspace too small: %zu < %zu", a->workspace_bytes,
