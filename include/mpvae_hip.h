@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 1
+#define MPV_ABI_VERSION 2
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -65,16 +65,21 @@ int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t
 int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* stream);
 
 /* 3xf16 split operand of the noise GEMMs: value = (hi + lo) / *scale, with hi
- * and lo fp16 planes of shape (rows_pad, ld), zero padded, and *scale a power
- * of two chosen on the device from max|x| (mpv_split_f16) or fixed
- * (mpv_noise_philox_f16).  hi*hi + hi*lo + lo*hi on the f16 matrix cores with
- * fp32 accumulation reproduces an fp32 product to ~2^-22. */
+ * and lo fp16 values, zero padded, and *scale a power of two chosen on the
+ * device from max|x| (mpv_split_f16) or fixed (mpv_noise_philox_f16).
+ * hi*hi + hi*lo + lo*hi on the f16 matrix cores with fp32 accumulation
+ * reproduces an fp32 product to ~2^-22.
+ *
+ * Chunked layout: row r is ld halves; every 32-column chunk k of the row is
+ * 32 hi halves followed by its 32 lo halves, so column c of row r has
+ *   hi at data[r*ld + (c/32)*64 + c%32],  lo 32 halves further,
+ * and one 128-B line carries both halves of a 32-element K slice (the GEMMs
+ * stream whole lines).  Columns 0 .. ld/2-1 are addressable. */
 typedef struct mpv_split16 {
-  uint16_t* hi;
-  uint16_t* lo;
+  uint16_t* data;
   float* scale;      /* device scalar */
   int64_t rows_pad;  /* allocated rows */
-  int64_t ld;        /* row length in elements, multiple of 8 */
+  int64_t ld;        /* halves per row: 2 x padded columns, a multiple of 64 */
 } mpv_split16;
 
 enum mpv_gemm { MPV_GEMM_F16X3 = 0, MPV_GEMM_F32 = 1 };
@@ -82,12 +87,14 @@ enum mpv_gemm { MPV_GEMM_F16X3 = 0, MPV_GEMM_F32 = 1 };
 size_t mpv_split_workspace_bytes(void);
 
 /* x (rows, cols) fp32 / fp64 -> split planes.  Used for r_sqrt_sigma
- * (replacing R.T.float(), mpvae.py:165) and for explicit noise. */
+ * (replacing R.T.float(), mpvae.py:165) and for explicit noise, which the
+ * caller passes as its (B, S_local, z) transpose (plane row b*S_local + s). */
 int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const mpv_split16* out,
                   void* workspace, void* stream);
 
-/* mpv_noise_philox writing split planes directly (rows = S_local*B, row = s*B+b);
- * the same numbers as mpv_noise_philox. */
+/* mpv_noise_philox writing split planes directly: S_local*B rows, plane row
+ * b*S_local + s = eps[s, b, :] (the s rows of one batch row contiguous, as the
+ * GEMMs stream them); the same numbers as mpv_noise_philox. */
 int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
                          const mpv_split16* out, void* stream);
 
@@ -104,8 +111,8 @@ typedef struct mpv_fwd_args {
   int gemm;             /* mpv_gemm: which operand pair below is used */
   const float* R32;     /* MPV_GEMM_F32:   (L,z) fp32 */
   const float* eps;     /*                 (S_local,B,z) fp32 */
-  mpv_split16 R16;      /* MPV_GEMM_F16X3: R planes, rows_pad >= roundup(L,128), ld >= roundup(z,128) */
-  mpv_split16 eps16;    /*                 noise planes, rows = S_local*B, ld as R16.ld */
+  mpv_split16 R16;      /* MPV_GEMM_F16X3: R planes, rows_pad >= roundup(L,128), ld >= 2*roundup(z,128) */
+  mpv_split16 eps16;    /*                 noise planes, row b*S_local + s = eps[s, b, :], ld as R16.ld */
   float* T;             /* (B,S_local,L) or NULL when no backward will follow */
   float* rowstat;       /* (6,B,S_local) out */
   float* bstat;         /* (6,B) out: this shard's statistics */

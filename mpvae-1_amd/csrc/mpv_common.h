@@ -140,6 +140,13 @@ MPV_DEV float pow2_scale(float maxabs) {
 
 MPV_DEV f16x8 as_f16x8(s16x8 v) { return __builtin_bit_cast(f16x8, v); }
 
+// Chunked split layout (include/mpvae_hip.h mpv_split16): index of the hi half
+// of column c in row r; the lo half is kLoOff further.
+constexpr int kLoOff = 32;
+__host__ __device__ inline int64_t chunked_index(int64_t r, int64_t ld, int64_t c) {
+  return r * ld + ((c >> 5) << 6) + (c & 31);
+}
+
 // ---- LDS-DMA pipelines: raw barrier + counted vmcnt ------------------------
 // __syncthreads() would make hipcc drain every in-flight LDS-DMA (vmcnt(0));
 // the rings use a raw s_barrier and wait for exactly the stages they read.
@@ -147,6 +154,13 @@ MPV_DEV void barrier_raw() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Barrier for LDS traffic only: this wave's LDS reads/writes are complete,
+// then every wave meets.  Unlike __syncthreads() it does not drain LDS-DMA.
+MPV_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier_raw();
 }
 
 template <int N>

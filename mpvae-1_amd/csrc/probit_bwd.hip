@@ -93,12 +93,11 @@ struct ElemParams {
   const float* gIL;  // (B,L) grad of indiv_prob_label (label branch) or NULL
   const float* coef;
   float* T;
-  uint16_t* g_hi;    // 3xf16 output planes (B*S rows, ldg), or NULL: fp32 G over T
-  uint16_t* g_lo;
+  uint16_t* g;       // chunked 3xf16 output planes (B*S rows of gld halves), or NULL: fp32 G over T
   const float* g_scale;
-  int64_t ldg;
+  int64_t gld;
   float* colpart;  // [nSc][2][B][L]
-  int S, B, L, Lc;  // Lc: columns covered (L, or ldg for planes: pads get zeros)
+  int S, B, L, Lc;  // Lc: columns covered (L, or gld/2 for planes: pads get zeros)
   int TPR, RPI, rows_per_chunk;
   float inv_S;
 };
@@ -176,9 +175,11 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
         uint16_t h[4], l[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
-        const int64_t o = ((int64_t)s * B + b) * p.ldg + c0;  // s-major rows; ldg % 4 == 0
-        *reinterpret_cast<s16x4*>(p.g_hi + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-        *reinterpret_cast<s16x4*>(p.g_lo + o) = s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+        // rows b*S + s (the noise planes' row order), chunked like mpv_split16
+        const int64_t o = chunked_index(cb, p.gld, c0);
+        *reinterpret_cast<s16x4*>(p.g + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+        *reinterpret_cast<s16x4*>(p.g + o + kLoOff) =
+            s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
       } else if (VEC && c0 + 3 < L) {
         *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
       } else {
@@ -211,29 +212,31 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
 }
 
 // ------------------------------------------------------------ 3xf16 dR GEMM
-// K axis = the S*B sample rows r = s*B + b: the noise planes' own row order, in
+// K axis = the S*B sample rows q = b*S + s: the noise planes' own row order, in
 // which the element pass also writes the G planes, so a K row is one address
-// for both operands.  The rows stream in stages of 32 through a 4-deep ring of
-// LDS buffers (LDS-DMA, 3 stages in flight, one barrier per stage).  Stage
-// image: [G_hi | G_lo | E_hi | E_lo], 32 rows x 128 columns x 2 B = 256 B per
-// row; the 32-B chunk c of row r sits at position c ^ (r & 7).  An MFMA
-// fragment (8 K rows of one column per lane) is two ds_read_b64_tr_b16; lane
-// group g reads rows 4g..4g+3 and 16+4g..16+4g+3, so a 32-lane half of one
-// transposed read touches rows 8j..8j+7 -> 8 distinct 32-B positions, all 64
-// banks once: conflict-free.  Element j of lane group g holds K row
-// (j < 4 ? 4g + j : 16 + 4g + j - 4), the same for A and B.
+// for both operands.  The rows stream in stages of 32 through a ring of LDS
+// stage images (LDS-DMA, one barrier per stage).  Both operands are chunked
+// (mpv_split16), so the 128 columns of a tile are 512 contiguous bytes per row
+// holding hi and lo; a stage image is [G rows | E rows], 32 rows x 512 B each,
+// and one DMA wave-instruction moves two whole rows.  The 32-B unit U of row r
+// (units 4k, 4k+1: hi of columns 32k..32k+31; 4k+2, 4k+3: their lo) sits at
+// position U ^ (r & 7).  An MFMA fragment (8 K rows of one column per lane) is
+// two ds_read_b64_tr_b16; lane group g reads rows 4g..4g+3 and 16+4g..16+4g+3,
+// so a 32-lane half of one transposed read touches rows 8j..8j+7 at 8 distinct
+// positions mod 256 B, all 64 banks once: conflict-free (checked).
+// Element j of lane group g holds K row (j < 4 ? 4g + j : 16 + 4g + j - 4), the
+// same for A and B.
 struct Dr16Params {
-  const uint16_t* g_hi;
-  const uint16_t* g_lo;
+  const uint16_t* g;    // chunked G planes, rows b*S + s, gld halves per row
   const float* g_scale;
-  int64_t ldg;          // G plane row length (>= nLt*128), rows s*B + b
-  mpv_split16 eps16;    // rows s*B + b, ld >= nZt*128
+  int64_t gld;
+  mpv_split16 eps16;    // rows b*S + s
   float* slab;          // [nKc][L][z]
   int S, B, L, z;
   int nLt, nZt, nKc, rows_per_chunk, rows_pad;
 };
 
-constexpr int kDrRowB = 256;  // bytes per LDS row (128 halves)
+constexpr int kDrRowB = 512;  // bytes per LDS row: 128 columns, hi + lo
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
@@ -255,23 +258,20 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
   }
 }
 
-// One stage's LDS-DMA for this wave: PER_WAVE 1-KB groups of 4 rows each,
-// written from `dst` on (wave-uniform).
+// One stage's LDS-DMA for this wave: PER_WAVE pieces of 2 rows x 512 B.  Wave
+// w moves pieces w*PER_WAVE ..; pieces 0..15 are G rows, 16..31 E rows.
 template <int PER_WAVE>
-MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, const int (&dma_r)[PER_WAVE],
-                      const int (&dma_off)[PER_WAVE], const int (&dma_plane)[PER_WAVE]) {
+MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
+                      const int (&dma_r)[PER_WAVE], const int (&dma_off)[PER_WAVE]) {
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
+    const int pc = wid * PER_WAVE + i;
     const int q = q0 + dma_r[i];
-    const uint16_t* src;
-    if (dma_plane[i] < 2) {
-      src = (dma_plane[i] ? p.g_lo : p.g_hi) + (int64_t)q * p.ldg;  // G rows >= rows are zero
-    } else {
-      src = (dma_plane[i] == 3 ? p.eps16.lo : p.eps16.hi) + (int64_t)min(q, rows - 1) * p.eps16.ld;
-    }
-    __builtin_amdgcn_global_load_lds(src + dma_off[i],
-                                     (__attribute__((address_space(3))) void*)(dst + i * 1024), 16,
-                                     0, 0);
+    const uint16_t* src = pc < 16 ? p.g + (int64_t)q * p.gld  // G rows >= rows are zero
+                                  : p.eps16.data + (int64_t)min(q, rows - 1) * p.eps16.ld;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + dma_off[i],
+                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
+                                     16, 0, 0);
   }
 }
 
@@ -279,12 +279,12 @@ template <int WM, int WN, int TM, int TN, int kDrStages>
 __global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
   constexpr int NW = WM * WN;
   constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
-  static_assert(BL == 128 && BZ == 128, "tile is 128 x 128 (one 256-B LDS row)");
-  constexpr int PLANE = kDrKR * kDrRowB;  // 8 KB
-  constexpr int STAGE = 4 * PLANE;        // 32 KB
-  constexpr int GROUPS = STAGE / 1024;    // 32 wave-instructions of 4 rows
-  static_assert(GROUPS % NW == 0, "DMA groups must split over waves");
-  constexpr int PER_WAVE = GROUPS / NW;
+  static_assert(BL == 128 && BZ == 128, "tile is 128 x 128 (one 512-B LDS row)");
+  constexpr int IMG = kDrKR * kDrRowB;  // 16 KB per operand
+  constexpr int STAGE = 2 * IMG;        // 32 KB
+  constexpr int PIECES = STAGE / 1024;  // 32 wave-instructions of 2 rows
+  static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
+  constexpr int PER_WAVE = PIECES / NW;
   constexpr int P = kDrStages - 1;
   __shared__ __attribute__((aligned(1024))) char smem[kDrStages * STAGE];
 
@@ -298,17 +298,16 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
   const int rows = p.B * p.S;
   const int q_begin = kc * p.rows_per_chunk;
   const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
-  // DMA lane mapping: 4 rows of 256 B per 1-KB wave-instruction; per-lane
-  // element offsets (without the stage's first row) of my PER_WAVE groups
-  const int dma_row = lane >> 4, dma_c = (lane & 15) >> 1, dma_half = lane & 1;
-  int dma_r[PER_WAVE], dma_off[PER_WAVE], dma_plane[PER_WAVE];
+  // DMA lane mapping: 2 rows of 512 B per wave-instruction; per-lane byte
+  // offsets (without the stage's first row) of my PER_WAVE pieces
+  int dma_r[PER_WAVE], dma_off[PER_WAVE];
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int grp = wid * PER_WAVE + i;
-    dma_plane[i] = grp >> 3;                    // 8 groups (32 rows) per plane
-    dma_r[i] = ((grp & 7) << 2) + dma_row;      // K row within the stage
-    const int col = ((dma_c ^ (dma_r[i] & 7)) << 4) + dma_half * 8;
-    dma_off[i] = (dma_plane[i] < 2 ? l0 : z0) + col;
+    const int pc = wid * PER_WAVE + i;
+    dma_r[i] = ((pc & 15) << 1) + (lane >> 5);  // K row within the stage
+    const int u_lds = (lane & 31) >> 1, half = lane & 1;
+    const int u_src = u_lds ^ (dma_r[i] & 7);
+    dma_off[i] = 2 * 2 * (pc < 16 ? l0 : z0) + u_src * 32 + half * 16;  // chunked column start: 2*col halves
   }
   // transposed-read lane mapping: lane 4q+p of its 16-lane group
   const int tq = lr >> 2, tp = lr & 3;
@@ -320,38 +319,37 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
 #pragma unroll
     for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-
   const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
   for (int j = 0; j < P && j < nst; ++j)
-    dr_issue<PER_WAVE>(p, smem + j * STAGE + wid * PER_WAVE * 1024, q_begin + j * kDrKR, rows,
-                       dma_r, dma_off, dma_plane);
+    dr_issue<PER_WAVE>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_r, dma_off);
   for (int ci = 0; ci < nst; ++ci) {
     wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
     if (ci + P < nst)
-      dr_issue<PER_WAVE>(p, smem + ((ci + P) % kDrStages) * STAGE + wid * PER_WAVE * 1024,
-                         q_begin + (ci + P) * kDrKR, rows, dma_r, dma_off, dma_plane);
+      dr_issue<PER_WAVE>(p, smem + ((ci + P) % kDrStages) * STAGE, q_begin + (ci + P) * kDrKR,
+                         rows, wid, dma_r, dma_off);
     const char* base = smem + (ci % kDrStages) * STAGE;
     s16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
     for (int m = 0; m < TM; ++m) {
-      const int cofs = (((wm * TM + m) ^ sw) << 5) + tp * 8;
-      ah[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + cofs),
-                                      tr_read(base, r1 * kDrRowB + cofs), 0, 1, 2, 3, 4, 5, 6, 7);
-      al[m] = __builtin_shufflevector(tr_read(base + PLANE, r0 * kDrRowB + cofs),
-                                      tr_read(base + PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3, 4,
-                                      5, 6, 7);
+      const int t = wm * TM + m, uh = (t >> 1) * 4 + (t & 1);
+      const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
+      ah[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + ch),
+                                      tr_read(base, r1 * kDrRowB + ch), 0, 1, 2, 3, 4, 5, 6, 7);
+      al[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + cl),
+                                      tr_read(base, r1 * kDrRowB + cl), 0, 1, 2, 3, 4, 5, 6, 7);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
-      const int cofs = (((wn * TN + n) ^ sw) << 5) + tp * 8;
-      bh[n] = __builtin_shufflevector(tr_read(base + 2 * PLANE, r0 * kDrRowB + cofs),
-                                      tr_read(base + 2 * PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3,
-                                      4, 5, 6, 7);
-      bl[n] = __builtin_shufflevector(tr_read(base + 3 * PLANE, r0 * kDrRowB + cofs),
-                                      tr_read(base + 3 * PLANE, r1 * kDrRowB + cofs), 0, 1, 2, 3,
-                                      4, 5, 6, 7);
+      const int t = wn * TN + n, uh = (t >> 1) * 4 + (t & 1);
+      const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
+      bh[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * kDrRowB + ch),
+                                      tr_read(base + IMG, r1 * kDrRowB + ch), 0, 1, 2, 3, 4, 5, 6,
+                                      7);
+      bl[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * kDrRowB + cl),
+                                      tr_read(base + IMG, r1 * kDrRowB + cl), 0, 1, 2, 3, 4, 5, 6,
+                                      7);
     }
 #pragma unroll
     for (int m = 0; m < TM; ++m)
@@ -533,7 +531,7 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
 struct BwdPlan {
   int TPR, RPI, nLc, nSc, rows_per_chunk;       // element pass
   int nLt, nZt, nKc, dr_rows_per_chunk, rows_pad;  // dR GEMM
-  int64_t ldg;                                  // G plane row length (3xf16)
+  int64_t ldg;                                  // G plane columns (3xf16, padded)
   size_t coef_bytes, colpart_bytes, slab_bytes, bound_bytes, planes_bytes;
 };
 
@@ -595,10 +593,11 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   const BwdPlan pl = plan_bwd(shape, a->gemm);
   if (a->dR32) {
     if (planes) {
-      MPV_REQUIRE(a->eps16.hi && a->eps16.lo && a->eps16.scale, "eps16 planes are NULL");
-      MPV_REQUIRE(a->eps16.ld >= (int64_t)pl.nZt * 128 && a->eps16.rows_pad >= shape->S_local * shape->B,
+      MPV_REQUIRE(a->eps16.data && a->eps16.scale, "eps16 planes are NULL");
+      MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * 128 && a->eps16.ld % 64 == 0 &&
+                      a->eps16.rows_pad >= shape->S_local * shape->B,
                   "eps16 planes too small (ld %lld < %lld)", (long long)a->eps16.ld,
-                  (long long)pl.nZt * 128);
+                  2 * (long long)pl.nZt * 128);
     } else {
       MPV_REQUIRE(a->eps != nullptr, "MPV_GEMM_F32 needs eps");
     }
@@ -614,9 +613,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   float* slab = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes);
   float* gbound = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes);
   float* gscale = gbound + shape->B;  // one float after the per-row bounds
-  uint16_t* g_hi = reinterpret_cast<uint16_t*>(ws + pl.coef_bytes + pl.colpart_bytes +
-                                               pl.slab_bytes + pl.bound_bytes);
-  uint16_t* g_lo = g_hi + (size_t)pl.rows_pad * pl.ldg;
+  // G planes, chunked: rows_pad rows of gld = 2 * ldg halves
+  uint16_t* g16 = reinterpret_cast<uint16_t*>(ws + pl.coef_bytes + pl.colpart_bytes +
+                                              pl.slab_bytes + pl.bound_bytes);
+  const int64_t gld = 2 * pl.ldg;
   const int S = (int)shape->S_local, B = (int)shape->B, L = (int)shape->L, z = (int)shape->z;
   const bool want_planes = planes && a->dR32 != nullptr;
 
@@ -628,9 +628,8 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
     if (int rc = launch_scale(gbound, B, gscale, st)) return rc;
     const int64_t pad_rows = (int64_t)pl.rows_pad - (int64_t)B * S;
     if (pad_rows > 0) {
-      const size_t off = (size_t)B * S * pl.ldg, n = (size_t)pad_rows * pl.ldg * sizeof(uint16_t);
-      if (hipMemsetAsync(g_hi + off, 0, n, st) != hipSuccess ||
-          hipMemsetAsync(g_lo + off, 0, n, st) != hipSuccess)
+      const size_t off = (size_t)B * S * gld, n = (size_t)pad_rows * gld * sizeof(uint16_t);
+      if (hipMemsetAsync(g16 + off, 0, n, st) != hipSuccess)
         return fail(MPV_ELAUNCH, "memset of G pad rows failed");
     }
   }
@@ -643,10 +642,9 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.gIL = a->g_indiv_label;
   ep.coef = coef;
   ep.T = a->T;
-  ep.g_hi = want_planes ? g_hi : nullptr;
-  ep.g_lo = want_planes ? g_lo : nullptr;
+  ep.g = want_planes ? g16 : nullptr;
   ep.g_scale = gscale;
-  ep.ldg = pl.ldg;
+  ep.gld = gld;
   ep.colpart = colpart;
   ep.S = S;
   ep.B = B;
@@ -673,10 +671,9 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
     const int64_t blocks = (int64_t)pl.nLt * pl.nZt * pl.nKc;
     if (planes) {
       Dr16Params dp;
-      dp.g_hi = g_hi;
-      dp.g_lo = g_lo;
+      dp.g = g16;
       dp.g_scale = gscale;
-      dp.ldg = pl.ldg;
+      dp.gld = gld;
       dp.eps16 = a->eps16;
       dp.slab = slab;
       dp.S = S;

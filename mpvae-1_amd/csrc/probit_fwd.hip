@@ -44,6 +44,10 @@ struct FwdParams {
   int nNt, nSc, tps, nSt;
 };
 
+#ifndef MPV_ABL
+#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
+#endif
+
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
 
@@ -67,59 +71,112 @@ MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
 // col = lane & 15 within each 16-wide tile), and its running column sums.
 template <int TN>
 struct FwdLane {
-  float fe[TN], fx[TN], y[TN], colE[TN], colEx[TN];
+  float colE[TN], colEx[TN];
+};
+
+template <int WN, int TN>
+MPV_DEV void fwd_lane_init(FwdLane<TN>& ln) {
+#pragma unroll
+  for (int n = 0; n < TN; ++n) ln.colE[n] = ln.colEx[n] = 0.0f;
+}
+
+// Label-column constants of the lane (fe_out, fx_out, y of its TN columns).
+template <int TN>
+struct FwdCols {
+  float fe[TN], fx[TN], y[TN];
   int col[TN];
   bool colok[TN], soft[TN];
 };
 
 template <int WN, int TN>
-MPV_DEV void fwd_lane_init(FwdLane<TN>& ln, const FwdParams& p, int b, int n0, int wn, int lr) {
+MPV_DEV void fwd_cols_load(FwdCols<TN>& c, const FwdParams& p, int b, int n0, int wn, int lr) {
 #pragma unroll
   for (int n = 0; n < TN; ++n) {
     const int col = n0 + wn * TN * 16 + n * 16 + lr;
-    ln.col[n] = col;
-    ln.colok[n] = col < p.L;
-    const int64_t o = (int64_t)b * p.L + (ln.colok[n] ? col : 0);
-    ln.y[n] = ln.colok[n] ? p.y[o] : 0.0f;
-    ln.fe[n] = ln.colok[n] ? p.fe[o] : 0.0f;
-    ln.fx[n] = ln.colok[n] ? p.fx[o] : 0.0f;
-    ln.soft[n] = !(ln.y[n] == 0.0f || ln.y[n] == 1.0f);
-    ln.colE[n] = ln.colEx[n] = 0.0f;
+    c.col[n] = col;
+    c.colok[n] = col < p.L;
+    const int64_t o = (int64_t)b * p.L + (c.colok[n] ? col : 0);
+    c.y[n] = p.y[o];
+    c.fe[n] = p.fe[o];
+    c.fx[n] = p.fx[o];
+    c.soft[n] = !(c.y[n] == 0.0f || c.y[n] == 1.0f);
   }
 }
 
-// One BM x BN tile of t (acc * scale): probit decode, row statistics written
-// to rowpart[., nt, b, s], column sums accumulated in `ln`.  Called by every
-// thread of the workgroup; uses `smem` (>= WN*BM*6 floats) after a barrier.
+// The same from an LDS copy cols[3][BN] (fe, fx, y of the workgroup's label
+// tile, staged once by fwd_cols_stage), so nothing is held in registers or
+// re-fetched from global memory across tiles.
+template <int WN, int TN>
+MPV_DEV void fwd_cols_lds(FwdCols<TN>& c, const float* cols, int L, int n0, int wn, int lr) {
+  constexpr int BN = WN * TN * 16;
+#pragma unroll
+  for (int n = 0; n < TN; ++n) {
+    const int cl = wn * TN * 16 + n * 16 + lr;
+    c.col[n] = n0 + cl;
+    c.colok[n] = n0 + cl < L;
+    c.fe[n] = cols[cl];
+    c.fx[n] = cols[BN + cl];
+    c.y[n] = cols[2 * BN + cl];
+    c.soft[n] = !(c.y[n] == 0.0f || c.y[n] == 1.0f);
+  }
+}
+
+template <int BN>
+MPV_DEV void fwd_cols_stage(float* cols, const FwdParams& p, int b, int n0, int nthreads) {
+  for (int i = threadIdx.x; i < BN; i += nthreads) {
+    const int col = n0 + i;
+    const bool ok = col < p.L;
+    const int64_t o = (int64_t)b * p.L + (ok ? col : 0);
+    cols[i] = ok ? p.fe[o] : 0.0f;
+    cols[BN + i] = ok ? p.fx[o] : 0.0f;
+    cols[2 * BN + i] = ok ? p.y[o] : 0.0f;
+  }
+}
+
+// One BM x BN tile of t (acc * scale) starting at sample row s0: probit
+// decode, row statistics written to rowpart[., nt, b, s], column sums
+// accumulated in `ln`, for the rows s_own <= s < S this tile owns.  Called by
+// every thread of the workgroup; uses `smem` (>= WN*BM*6 floats).
 template <int WM, int WN, int TM, int TN>
 MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)[TM][TN],
-                               float scale, int b, int s0, int nt, float* smem) {
-  constexpr int NT = WM * WN * 64, BM = WM * TM * 16;
+                               float scale, int b, int s0, int s_own, int nt, float* smem,
+                               const float* cols = nullptr) {
+  constexpr int NT = WM * WN * 64, BM = WM * TM * 16, BN = WN * TN * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN, lr = lane & 15, lg = lane >> 4;
   const int S = p.S, B = p.B, L = p.L;
+  FwdCols<TN> cl;
+  if (cols != nullptr) {
+    // opaque per call: keeps the column constants (and everything derived
+    // from them) from being hoisted out of the tile loop into registers that
+    // would then live across the main loop
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    fwd_cols_lds<WN, TN>(cl, cols + zero, L, nt * BN + zero, wn, lr);
+  } else
+    fwd_cols_load<WN, TN>(cl, p, b, nt * BN, wn, lr);
   float* red = smem;  // [WN][BM][6]
-  __syncthreads();    // the main loop's last LDS reads are done before red is written
+  lds_barrier();      // the main loop's last LDS reads are done before red is written
 #pragma unroll
   for (int m = 0; m < TM; ++m) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rl = wm * TM * 16 + m * 16 + lg * 4 + i;
       const int s = s0 + rl;
-      const bool rowok = s < S;
+      const bool rowok = s >= s_own && s < S;
       float st6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
-        const bool ok = rowok && ln.colok[n];
+        const bool ok = rowok && cl.colok[n];
         const float t = acc[m][n][i] * scale;
-        if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + ln.col[n]] = t;
-        const float E = probit_prob(t + ln.fe[n]);
-        const float Ex = probit_prob(t + ln.fx[n]);
-        const float y = ln.y[n];
+        if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + cl.col[n]] = t;
+        const float E = probit_prob(t + cl.fe[n]);
+        const float Ex = probit_prob(t + cl.fx[n]);
+        const float y = cl.y[n];
         // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
         float le = fast_log(y == 0.0f ? 1.0f - E : E);
         float lx = fast_log(y == 0.0f ? 1.0f - Ex : Ex);
-        if (ln.soft[n]) {
+        if (cl.soft[n]) {
           le = y * fast_log(E) + (1.0f - y) * fast_log(1.0f - E);
           lx = y * fast_log(Ex) + (1.0f - y) * fast_log(1.0f - Ex);
         }
@@ -147,10 +204,10 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one m-slab
   }
-  __syncthreads();
+  lds_barrier();
   for (int r = tid; r < BM; r += NT) {
     const int s = s0 + r;
-    if (s < S) {
+    if (s >= s_own && s < S) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         float v = 0.0f;
@@ -160,7 +217,7 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // Column sums of this workgroup -> colpart[sc, ., b, n0 ...].
@@ -225,7 +282,7 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
   const bool zvec = (z & 3) == 0;
 
   FwdLane<TN> ln;
-  fwd_lane_init<WN, TN>(ln, p, b, n0, wn, lr);
+  fwd_lane_init<WN, TN>(ln);
 
   const int nK = (z + kBK - 1) / kBK;
   const int st_end = min(p.nSt, (sc + 1) * p.tps);
@@ -325,51 +382,174 @@ __global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
         __syncthreads();
       }
     }
-    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, 1.0f, b, s0, nt, smem);
+    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, 1.0f, b, s0, s0, nt, smem);
   }
   fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, smem);
 }
 
 // ------------------------------------------------------ 3xf16 mainloop
-// The K axis (z) is streamed in stages of 32 halves (one MFMA k-step) through a
-// ring of NSTAGE LDS buffers filled by LDS-DMA (global_load_lds_dwordx4), with
-// NSTAGE-1 stages in flight and one barrier per stage.  Stage image:
-// [A_hi | A_lo | B_hi | B_lo], each row 64 B; the 16-B chunk c of row r sits at
-// position c ^ ((r >> 1) & 3), which makes the ds_read_b128 fragment reads
-// (16 rows x one 16-B column per lane group) hit 16 distinct slots of the
-// 256-B bank row (exhaustively checked).  LDS-DMA writes
-// lane-linearly, so the swizzle goes on the per-lane SOURCE address and the
-// same XOR is applied on the read.
-constexpr int kKC = 32;    // K halves per stage
-constexpr int kRowB = 64;  // bytes per plane row per stage
+// The K axis (z) is streamed in stages of 32 (one MFMA k-step) through a ring
+// of NSTAGE LDS stage images filled by LDS-DMA (global_load_lds_dwordx4).  The
+// split operands are chunked (mpv_split16): the hi and lo halves of a row's
+// 32-element K slice are one 128-B line, and a stage image row is exactly that
+// line: [hi 64 B | lo 64 B].  Image: BM eps rows (A), then BN R rows (B).  One
+// DMA wave-instruction moves 8 rows (8 lanes x 16 B per row: whole lines).
+// The 16-B unit u of row r sits at position u ^ ((r >> 1) & 7), which makes
+// the ds_read_b128 fragment reads (16 rows x one unit per lane group)
+// conflict-free (checked exhaustively); LDS-DMA writes
+// lane-linearly, so the swizzle goes on the per-lane SOURCE address.
+constexpr int kKC = 32;     // K elements per stage
+constexpr int kRowB = 128;  // bytes per stage-image row (hi + lo)
 
-// One K stage (k0 halves in) of this wave's DMA groups into stage image `dst`.
-// A device function rather than a lambda: hipcc drops the host stub of a
-// template kernel whose lambda captures arrays.
-template <int GMAX, int GROUPS, int NW>
-MPV_DEV void fwd16_issue(char* dst, int k0, int wid, const char* const (&gbase)[GMAX],
-                         const uint32_t (&goff)[GMAX]) {
+// First sample row of s-tile st.  With S >= BM the last tile is shifted back
+// to end at S (its leading rows, already owned by tile st-1, are recomputed
+// and masked), so no tile reads past the last sample row and the per-lane DMA
+// offsets are the same for every tile; with S < BM rows are clamped instead.
+template <int BM>
+MPV_DEV int fwd_tile_s0(int st, int S) {
+  return S >= BM ? min(st * BM, S - BM) : 0;
+}
+
+// DMA cursor of one wave: the next K stage to stream, walking the stages of
+// every tile this workgroup owns in order (so the first stages of tile i+1
+// are fetched while tile i's epilogue runs).  Wave w streams the 8-row pieces
+// w, w+NW, ... of each operand image.  A source address is a wave-uniform
+// operand/tile base plus a tile-invariant 32-bit per-lane byte offset.
+template <int BM, int BN, int NW>
+struct Fwd16Dma {
+  static constexpr int GA = BM / 8, GB = BN / 8;  // pieces per operand image
+  static constexpr int JA = (GA + NW - 1) / NW, JB = (GB + NW - 1) / NW;
+  static constexpr bool EVEN = GA % NW == 0 && GB % NW == 0;
+  const char* a_base;  // eps rows of the current tile
+  const char* b_base;  // R rows of the label tile
+  uint32_t offa[JA], offb[JB];
+  int tile, kc;  // next stage to issue
+  int issued;    // stages issued so far
+  int wid;
+
+  MPV_DEV void init(const FwdParams& p, int t0, int b, int n0, int wid_, int lane) {
+    wid = wid_;
+    const int64_t lda = p.eps16.ld, ldb = p.R16.ld;
+    const int prow = lane >> 3, u_lds = lane & 7;
+    b_base = reinterpret_cast<const char*>(p.R16.data + (int64_t)n0 * ldb);
 #pragma unroll
-  for (int i = 0; i < GMAX; ++i) {
-    const int grp = wid + i * NW;
-    if (GROUPS % NW != 0 && grp >= GROUPS) break;
-    __builtin_amdgcn_global_load_lds(gbase[i] + 2 * k0 + goff[i],
-                                     (__attribute__((address_space(3))) void*)(dst + grp * 1024),
-                                     16, 0, 0);
+    for (int j = 0; j < JA; ++j) {
+      const int r = (wid + j * NW) * 8 + prow;  // row within the tile
+      offa[j] = (uint32_t)((int64_t)min(r, p.S - 1) * lda * 2) +  // rows b*S + s: contiguous
+                (uint32_t)((u_lds ^ ((r >> 1) & 7)) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int r = (wid + j * NW) * 8 + prow;
+      offb[j] = (uint32_t)(r * ldb * 2) + (uint32_t)((u_lds ^ ((r >> 1) & 7)) * 16);
+    }
+    tile = t0;
+    kc = 0;
+    issued = 0;
+    set_tile(p, b);
+  }
+
+  MPV_DEV void set_tile(const FwdParams& p, int b) {
+    const int64_t o = ((int64_t)b * p.S + fwd_tile_s0<BM>(tile, p.S)) * p.eps16.ld;
+    a_base = reinterpret_cast<const char*>(p.eps16.data + o);
+  }
+
+  // pieces this wave streams per stage
+  MPV_DEV int per_wave() const {
+    if (EVEN) return JA + JB;
+    return (GA - wid + NW - 1) / NW + (GB - wid + NW - 1) / NW;
+  }
+
+  MPV_DEV static void piece(const char* src, char* dst) {
+    if (MPV_ABL & 4) return;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+
+  // Stream the next stage (if any) into stage image `dst`.
+  MPV_DEV void issue(const FwdParams& p, char* dst, int tile_end, int nK, int b) {
+    if (tile >= tile_end) return;
+    const int kb = kc * kRowB;  // byte offset of the K slice within a row
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const int pc = wid + j * NW;
+      if (GA % NW == 0 || pc < GA) piece(a_base + kb + offa[j], dst + pc * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int pc = wid + j * NW;
+      if (GB % NW == 0 || pc < GB) piece(b_base + kb + offb[j], dst + BM * kRowB + pc * 1024);
+    }
+    ++issued;
+    if (++kc == nK) {
+      kc = 0;
+      if (++tile < tile_end) set_tile(p, b);
+    }
+  }
+};
+
+// Operand fragments of one K stage: A (eps rows) and B (R rows), hi and lo.
+template <int TM, int TN>
+struct Frag16 {
+  s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+};
+
+// coh / col: swizzled byte positions of this lane's hi and lo units
+template <int TM, int TN, int BM>
+MPV_DEV void fwd16_read(Frag16<TM, TN>& f, const char* base, int wm, int wn, int lr, int coh,
+                        int col) {
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const int off = ((wm * TM + m) * 16 + lr) * kRowB;
+    f.ah[m] = *reinterpret_cast<const s16x8*>(base + off + coh);
+    f.al[m] = *reinterpret_cast<const s16x8*>(base + off + col);
+  }
+#pragma unroll
+  for (int n = 0; n < TN; ++n) {
+    const int off = (BM + (wn * TN + n) * 16 + lr) * kRowB;
+    f.bh[n] = *reinterpret_cast<const s16x8*>(base + off + coh);
+    f.bl[n] = *reinterpret_cast<const s16x8*>(base + off + col);
   }
 }
 
+// acc += hi*hi + hi*lo + lo*hi for one K stage.
+template <int TM, int TN>
+MPV_DEV void fwd16_mfma(f32x4 (&acc)[TM][TN], const Frag16<TM, TN>& f) {
+  if (MPV_ABL & 16) {
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+        acc[m][n][0] += __builtin_bit_cast(float, __builtin_shufflevector(f.ah[m], f.bl[n], 0, 8)) +
+                        __builtin_bit_cast(float, __builtin_shufflevector(f.al[m], f.bh[n], 0, 8));
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
+                                                         acc[m][n], 0, 0, 0);
+    }
+}
+
+// Main loop: a ring of NSTAGE stage images, NSTAGE-1 stages in flight, one
+// raw barrier per stage (the DMA stream runs across tile seams).
 template <int WM, int WN, int TM, int TN, int NSTAGE>
 __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fwd16_kernel(FwdParams p) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
-  constexpr int PLANE_A = BM * kRowB, PLANE_B = BN * kRowB;
-  constexpr int STAGE = 2 * PLANE_A + 2 * PLANE_B;
-  static_assert(STAGE % 1024 == 0, "stage must be whole 1-KB DMA groups");
-  constexpr int GROUPS = STAGE / 1024;  // 16 rows each
-  constexpr int GMAX = (GROUPS + NW - 1) / NW;
-  constexpr int P = NSTAGE - 1;         // stages in flight
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE];
+  constexpr int STAGE = (BM + BN) * kRowB;
+  static_assert(BM % 8 == 0 && BN % 8 == 0, "operand images are whole 8-row DMA pieces");
+  constexpr int RED = (WN * BM * 6 > WM * BN * 2 ? WN * BM * 6 : WM * BN * 2) * 4;
+  // one __shared__ array: stage ring, the epilogue's reduction area, and the
+  // label tile's fe/fx/y
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + RED + 3 * BN * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cols = reinterpret_cast<float*>(smem + NSTAGE * STAGE + RED);
 
   int g, nt;
   decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
@@ -379,95 +559,57 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.S, B = p.B;
-  const int64_t lda = p.eps16.ld, ldb = p.R16.ld;
 
   FwdLane<TN> ln;
-  fwd_lane_init<WN, TN>(ln, p, b, n0, wn, lr);
+  fwd_lane_init<WN, TN>(ln);
   const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
   const int nK = (p.z + kKC - 1) / kKC;
-  const int coff = (lg ^ ((lr >> 1) & 3)) << 4;  // swizzled 16-B column of this lane's reads
-  const int my_groups = (GROUPS - wid + NW - 1) / NW;
-  const int dma_row = lane >> 2, dma_pos = lane & 3;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
 
-  const int st_end = min(p.nSt, (sc + 1) * p.tps);
-  for (int st = sc * p.tps; st < st_end; ++st) {
-    const int s0 = st * BM;
-    // DMA sources of this wave's groups (wid, wid+NW, ... of 16 rows; a group
-    // never straddles planes): a wave-uniform 64-bit plane/tile base plus a
-    // 32-bit per-lane byte offset (row within the tile, swizzled chunk), so
-    // the loop carries one VGPR per group and issues the saddr form.
-    const char* gbase[GMAX];
-    uint32_t goff[GMAX];
+  fwd_cols_stage<BN>(cols, p, b, n0, NW * 64);  // visible after the first barrier
+  Fwd16Dma<BM, BN, NW> dma;
+  dma.init(p, t_begin, b, n0, wid, lane);
+  const int my_pieces = dma.per_wave();
 #pragma unroll
-    for (int i = 0; i < GMAX; ++i) {
-      const int grp = min(wid + i * NW, GROUPS - 1);
-      const int row0 = grp * 16;  // wave-uniform first row of the group
-      const int r16 = dma_row;
-      int r;
-      if (row0 < 2 * BM) {
-        const int plane = row0 >= BM;
-        const int rb = row0 - plane * BM;  // uniform
-        r = rb + r16;
-        const int s = min(s0 + r, S - 1);
-        gbase[i] = reinterpret_cast<const char*>((plane ? p.eps16.lo : p.eps16.hi) +
-                                                 ((int64_t)s0 * B + b) * lda);
-        goff[i] = (uint32_t)((int64_t)(s - s0) * B * lda * 2);
-      } else {
-        const int plane = row0 >= 2 * BM + BN;
-        const int rb = row0 - 2 * BM - plane * BN;
-        r = rb + r16;
-        gbase[i] = reinterpret_cast<const char*>((plane ? p.R16.lo : p.R16.hi) +
-                                                 (int64_t)n0 * ldb);
-        goff[i] = (uint32_t)(r * ldb * 2);
-      }
-      goff[i] += (uint32_t)((dma_pos ^ ((r >> 1) & 3)) * 16);
-    }
+  for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
 
+  int gs = 0;  // stages consumed so far (global over the tiles)
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int j = 0; j < P && j < nK; ++j) fwd16_issue<GMAX, GROUPS, NW>(smem + j * STAGE, j * kKC, wid, gbase, goff);
-    for (int kc = 0; kc < nK; ++kc) {
-      // stages issued after kc may stay in flight; kc itself must have landed
-      wait_vmcnt_dyn(min(P - 1, nK - 1 - kc) * my_groups);
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
+      // stage gs must have landed; later stages may stay in flight (loads
+      // retire in order, so stores issued after them need not be waited for)
+      if (NSTAGE == 2)
+        wait_vmcnt<0>();
+      else
+        wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * my_pieces);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier_raw();  // kc landed for every wave; every wave is done reading kc-1
-      if (kc + P < nK) fwd16_issue<GMAX, GROUPS, NW>(smem + ((kc + P) % NSTAGE) * STAGE, (kc + P) * kKC, wid,
-                                                gbase, goff);
-      const char* base = smem + (kc % NSTAGE) * STAGE;
-      s16x8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int m = 0; m < TM; ++m) {
-        const int off = ((wm * TM + m) * 16 + lr) * kRowB + coff;
-        ah[m] = *reinterpret_cast<const s16x8*>(base + off);
-        al[m] = *reinterpret_cast<const s16x8*>(base + PLANE_A + off);
-      }
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int off = 2 * PLANE_A + ((wn * TN + n) * 16 + lr) * kRowB + coff;
-        bh[n] = *reinterpret_cast<const s16x8*>(base + off);
-        bl[n] = *reinterpret_cast<const s16x8*>(base + PLANE_B + off);
-      }
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+      Frag16<TM, TN> f;
+      fwd16_read<TM, TN, BM>(f, smem + (gs % NSTAGE) * STAGE, wm, wn, lr, coh, col);
+      fwd16_mfma<TM, TN>(acc, f);
+    }
+    if (MPV_ABL & 1) {
+      float v = 0.f;
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int n = 0; n < TN; ++n) {
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
-                                                             acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
-                                                             acc[m][n], 0, 0, 0);
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(al[m]), as_f16x8(bh[n]),
-                                                             acc[m][n], 0, 0, 0);
-        }
+        for (int n = 0; n < TN; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
+    } else {
+      fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, st * BM, nt, red, cols);
     }
-    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, nt,
-                                      reinterpret_cast<float*>(smem));
   }
-  fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, reinterpret_cast<float*>(smem));
+  fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, red);
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
@@ -632,11 +774,12 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
 
 static int check_split_operand(const mpv_split16& o, int64_t rows, int64_t ld_min,
                                const char* what) {
-  MPV_REQUIRE(o.hi && o.lo && o.scale, "%s: NULL plane", what);
+  MPV_REQUIRE(o.data && o.scale, "%s: NULL plane", what);
   MPV_REQUIRE(o.rows_pad >= rows, "%s: rows_pad %lld < %lld", what, (long long)o.rows_pad,
               (long long)rows);
-  MPV_REQUIRE(o.ld >= ld_min && (o.ld % 8) == 0, "%s: ld %lld must be >= %lld and a multiple of 8",
-              what, (long long)o.ld, (long long)ld_min);
+  MPV_REQUIRE(o.ld >= ld_min && (o.ld % 64) == 0,
+              "%s: ld %lld must be >= %lld and a multiple of 64", what, (long long)o.ld,
+              (long long)ld_min);
   return MPV_OK;
 }
 
@@ -664,13 +807,13 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   if (a->gemm == MPV_GEMM_F32) {
     MPV_REQUIRE(a->R32 && a->eps, "MPV_GEMM_F32 needs R32 and eps");
   } else {
-    const int64_t zp = cdiv(shape->z, 64) * 64;
-    if (int rc = check_split_operand(a->R16, (int64_t)pl.nNt * pl.BN, zp, "R16")) return rc;
-    if (int rc = check_split_operand(a->eps16, shape->S_local * shape->B, zp, "eps16")) return rc;
+    const int64_t ldk = 2 * cdiv(shape->z, kKC) * kKC;  // K slices the main loop reads
+    if (int rc = check_split_operand(a->R16, (int64_t)pl.nNt * pl.BN, ldk, "R16")) return rc;
+    if (int rc = check_split_operand(a->eps16, shape->S_local * shape->B, ldk, "eps16")) return rc;
     // the DMA issue keeps per-lane byte offsets within one s/l tile in 32 bits
-    MPV_REQUIRE((int64_t)pl.BM * shape->B * a->eps16.ld * 2 < (int64_t(1) << 32) &&
+    MPV_REQUIRE((int64_t)pl.BM * a->eps16.ld * 2 < (int64_t(1) << 32) &&
                     (int64_t)pl.BN * a->R16.ld * 2 < (int64_t(1) << 32),
-                "B * ld too large for the f16x3 tile offsets");
+                "ld too large for the f16x3 tile offsets");
   }
   MPV_REQUIRE(a->workspace_bytes >= pl.rowpart_bytes + pl.colpart_bytes,
               "workspace too small: %zu < %zu", a->workspace_bytes,

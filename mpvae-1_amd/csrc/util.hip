@@ -235,36 +235,43 @@ __global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ bl
   if (threadIdx.x == 0) *scale = pow2_scale(m);
 }
 
-// (rows, cols) row-major -> hi/lo planes (rows_pad, ld), zero padded.
+// (rows, cols) row-major -> chunked split planes (rows_pad x ld/2 columns),
+// zero padded.  Thread i owns logical element (r, c) = (i / cols_pad, i % cols_pad).
 template <typename T>
 __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int64_t rows,
                                                    int64_t cols, mpv_split16 out) {
   const float s = *out.scale;
-  const int64_t n = out.rows_pad * out.ld;
+  const int64_t cp = out.ld >> 1;
+  const int64_t n = out.rows_pad * cp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / out.ld, c = i - r * out.ld;
+    const int64_t r = i / cp, c = i - r * cp;
     const float v = (r < rows && c < cols) ? (float)x[r * cols + c] : 0.0f;
     uint16_t h, l;
     split_f16(v, s, h, l);
-    out.hi[i] = h;
-    out.lo[i] = l;
+    const int64_t o = chunked_index(r, out.ld, c);
+    out.data[o] = h;
+    out.data[o + kLoOff] = l;
   }
 }
 
-// Philox noise straight into 3xf16 planes: row = s*B + b (padded to ld).
+// Philox noise straight into 3xf16 planes: plane row r = b*S_local + s holds
+// the noise of (s, b) (same values as the fp32 (S, B, z) draw, rows reordered
+// so that the s rows of one batch row are contiguous for the GEMMs).
 // Box-Muller output is bounded by sqrt(-2 ln 2^-25) < 5.9, so the scale is
 // the constant 2^12 (max |n| * s < 24200 < 65504).
 constexpr float kNoiseScale = 4096.0f;
 
-__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int64_t rows,
-                                                            int64_t z, int64_t e_row0,
+__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int64_t S,
+                                                            int64_t B, int64_t z, int64_t s_off,
                                                             uint32_t k0, uint32_t k1,
                                                             uint64_t offset) {
-  const int64_t q4 = out.ld >> 2;
+  const int64_t q4 = out.ld >> 3;  // 4-column groups per row
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows * q4) return;
+  if (i >= S * B * q4) return;
   const int64_t r = i / q4, c0 = (i - r * q4) * 4;
+  const int64_t bb = r / S, ss = r - bb * S;
+  const int64_t e_row = (s_off + ss) * B + bb;  // row of the global (S_total, B, z) draw
   uint64_t cached = ~0ull;
   u32x4 w = {0u, 0u, 0u, 0u};
   uint16_t h[4], l[4];
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
     const int64_t c = c0 + q;
     float v = 0.0f;
     if (c < z) {
-      const int64_t e = (e_row0 + r) * z + c;  // global element index
+      const int64_t e = e_row * z + c;  // global element index
       const uint64_t g = (uint64_t)(e >> 2);
       if (g != cached) {
         const uint64_t ctr = g + offset;
@@ -288,9 +295,10 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
     }
     split_f16(v, kNoiseScale, h[q], l[q]);
   }
-  const int64_t o = r * out.ld + c0;
-  *reinterpret_cast<s16x4*>(out.hi + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-  *reinterpret_cast<s16x4*>(out.lo + o) = s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+  const int64_t o = chunked_index(r, out.ld, c0);
+  *reinterpret_cast<s16x4*>(out.data + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+  *reinterpret_cast<s16x4*>(out.data + o + kLoOff) =
+      s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
 }
 
 __global__ void set_scalar_kernel(float* p, float v) { *p = v; }
@@ -369,9 +377,9 @@ int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* 
 }
 
 static int check_split(const mpv_split16* o) {
-  MPV_REQUIRE(o && o->hi && o->lo && o->scale, "NULL pointer in mpv_split16");
-  MPV_REQUIRE(o->rows_pad > 0 && o->ld > 0 && (o->ld % 8) == 0, "mpv_split16: ld must be a "
-              "positive multiple of 8 (got %lld)", (long long)o->ld);
+  MPV_REQUIRE(o && o->data && o->scale, "NULL pointer in mpv_split16");
+  MPV_REQUIRE(o->rows_pad > 0 && o->ld > 0 && (o->ld % 64) == 0, "mpv_split16: ld must be a "
+              "positive multiple of 64 (got %lld)", (long long)o->ld);
   return MPV_OK;
 }
 
@@ -381,7 +389,7 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
                   void* workspace, void* stream) {
   if (int rc = check_split(out)) return rc;
   MPV_REQUIRE(x && workspace && rows > 0 && cols > 0, "bad mpv_split_f16 arguments");
-  MPV_REQUIRE(rows <= out->rows_pad && cols <= out->ld, "planes smaller than the input");
+  MPV_REQUIRE(rows <= out->rows_pad && cols <= out->ld / 2, "planes smaller than the input");
   MPV_REQUIRE(x_dtype == MPV_F32 || x_dtype == MPV_F64, "unsupported dtype %d", x_dtype);
   hipStream_t s = as_stream(stream);
   float* bmax = reinterpret_cast<float*>(workspace);
@@ -392,7 +400,7 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
   else
     MPV_LAUNCH("split", maxabs_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, n, bmax);
   MPV_LAUNCH("split", scale_kernel, dim3(1), dim3(256), 0, s, bmax, (int)g, out->scale);
-  const unsigned g2 = grid_for(out->rows_pad * out->ld, 256, 16384);
+  const unsigned g2 = grid_for(out->rows_pad * (out->ld / 2), 256, 16384);
   if (x_dtype == MPV_F64)
     MPV_LAUNCH("split", split_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)x, rows,
                cols, *out);
@@ -407,13 +415,13 @@ int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
   if (int rc = check_shape(shape)) return rc;
   if (int rc = check_split(out)) return rc;
   const int64_t rows = shape->S_local * shape->B;
-  MPV_REQUIRE(out->rows_pad >= rows && out->ld >= shape->z, "noise planes too small");
+  MPV_REQUIRE(out->rows_pad >= rows && out->ld / 2 >= shape->z, "noise planes too small");
   hipStream_t s = as_stream(stream);
   MPV_LAUNCH("noise_philox", set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
-  const int64_t n = rows * (out->ld / 4);
+  const int64_t n = rows * (out->ld / 8);
   MPV_REQUIRE(cdiv(n, 256) < (int64_t(1) << 31), "noise too large");
   MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
-             *out, rows, shape->z, shape->s_offset * shape->B, (uint32_t)seed,
+             *out, shape->S_local, shape->B, shape->z, shape->s_offset, (uint32_t)seed,
              (uint32_t)(seed >> 32), offset);
   return check_launch("noise_philox_f16");
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -32,7 +32,8 @@ class Shape(ctypes.Structure):
 
 
 class Split16(ctypes.Structure):
-    _fields_ = [("hi", vp), ("lo", vp), ("scale", vp), ("rows_pad", ctypes.c_int64),
+    """mpv_split16: chunked hi/lo planes (include/mpvae_hip.h)."""
+    _fields_ = [("data", vp), ("scale", vp), ("rows_pad", ctypes.c_int64),
                 ("ld", ctypes.c_int64)]
 
 

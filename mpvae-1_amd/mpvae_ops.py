@@ -27,23 +27,30 @@ def _pad(n, m):
 
 
 class Planes:
-    """3xf16 split operand (include/mpvae_hip.h mpv_split16): value = (hi + lo) / scale,
-    hi/lo fp16 planes of shape (rows_pad, ld), zero padded."""
+    """3xf16 split operand (include/mpvae_hip.h mpv_split16) of `cols` padded
+    columns: value = (hi + lo) / scale, stored chunked -- every 32-column chunk
+    of a row is 32 hi halves then 32 lo halves (row length ld = 2 * cols)."""
 
-    def __init__(self, rows_pad, ld, device):
-        self.rows_pad, self.ld = int(rows_pad), int(ld)
-        self.hi = torch.empty((self.rows_pad, self.ld), dtype=torch.int16, device=device)
-        self.lo = torch.empty_like(self.hi)
+    def __init__(self, rows_pad, cols, device):
+        if cols % 32:
+            raise ValueError(f"split planes need a multiple of 32 columns (got {cols})")
+        self.rows_pad, self.cols, self.ld = int(rows_pad), int(cols), 2 * int(cols)
+        self.data = torch.empty((self.rows_pad, self.ld), dtype=torch.int16, device=device)
         self.scale = torch.empty((1,), dtype=torch.float32, device=device)
 
     def c(self):
-        return H.Split16(self.hi.data_ptr(), self.lo.data_ptr(), self.scale.data_ptr(),
-                         self.rows_pad, self.ld)
+        return H.Split16(self.data.data_ptr(), self.scale.data_ptr(), self.rows_pad, self.ld)
+
+    def halves(self):
+        """(hi, lo) as (rows_pad, cols) fp16 views' fp32 values."""
+        v = self.data.view(torch.float16).float().view(self.rows_pad, self.cols // 32, 2, 32)
+        return v[:, :, 0, :].reshape(self.rows_pad, self.cols), \
+            v[:, :, 1, :].reshape(self.rows_pad, self.cols)
 
     def value(self):
         """fp32 value of the planes (tests / diagnostics)."""
-        return (self.hi.view(torch.float16).float() + self.lo.view(torch.float16).float()) \
-            / self.scale
+        hi, lo = self.halves()
+        return (hi + lo) / self.scale
 
 
 GEMMS = {"f16x3": H.GEMM_F16X3, "f32": H.GEMM_F32}
@@ -87,7 +94,9 @@ class HipShardBackend:
         if self.gemm == H.GEMM_F32:
             return eps
         rows = shape.S_local * shape.B
-        return self._split(eps, rows, shape.z, Planes(rows, _pad(shape.z, 128), eps.device))
+        # plane rows are b-major (row b*S + s): split the (B, S, z) transpose
+        eps_bs = eps.transpose(0, 1).contiguous()
+        return self._split(eps_bs, rows, shape.z, Planes(rows, _pad(shape.z, 128), eps.device))
 
     def prepare_R(self, R):
         """r_sqrt_sigma (L,z) fp64/fp32 -> the GEMM operand (R.T.float(), mpvae.py:165)."""

@@ -100,8 +100,10 @@ def test_philox_noise_matches_oracle(S, B, z, s_off):
     # the 3xf16 planes hold the same numbers (to the split's 2^-22) and zero padding
     pl = HipShardBackend("f16x3").make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
     v = _np(pl.value())
-    assert v.shape == (S * B, pl.ld) and pl.ld % 128 == 0
-    np.testing.assert_allclose(v[:, :z].reshape(S, B, z), ref, atol=2e-5, rtol=2e-5)
+    assert v.shape == (S * B, pl.cols) and pl.cols % 128 == 0 and pl.ld == 2 * pl.cols
+    # plane row b*S + s holds eps[s, b]
+    np.testing.assert_allclose(v[:, :z].reshape(B, S, z).transpose(1, 0, 2), ref, atol=2e-5,
+                               rtol=2e-5)
     assert not v[:, z:].any()
 
 
@@ -112,7 +114,7 @@ def test_split_planes_round_trip():
     for scale in (1e-6, 0.05, 3.0, 2e4):
         R = torch.randn((37, 53), device=DEV, dtype=torch.float64, generator=g) * scale
         pl = be.prepare_R(R)
-        assert pl.rows_pad == 128 and pl.ld == 128
+        assert pl.rows_pad == 128 and pl.cols == 128 and pl.ld == 256
         v = pl.value().double()
         err = (v[:37, :53] - R).abs().max() / R.abs().max()
         assert float(err) < 1e-6, (scale, float(err))
