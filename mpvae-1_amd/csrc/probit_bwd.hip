@@ -236,10 +236,18 @@ struct Dr16Params {
   int nLt, nZt, nKc, rows_per_chunk, rows_pad;
 };
 
-constexpr int kDrRowB = 512;  // bytes per LDS row: 128 columns, hi + lo
+#ifndef MPV_ABL
+#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
+#endif
+
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
+  if (MPV_ABL & 256) {
+    s16x4 v = s16x4{(short)off, 1, 2, 3};
+    asm volatile("" : "+v"(v));
+    return v;
+  }
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) s16x4*)(base + off));
 }
@@ -258,17 +266,19 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
   }
 }
 
-// One stage's LDS-DMA for this wave: PER_WAVE pieces of 2 rows x 512 B.  Wave
-// w moves pieces w*PER_WAVE ..; pieces 0..15 are G rows, 16..31 E rows.
-template <int PER_WAVE>
+// One stage's LDS-DMA for this wave: PER_WAVE 1-KB pieces (whole rows).
+// Wave w moves pieces w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E.
+template <int PER_WAVE, int PIECES>
 MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
                       const int (&dma_r)[PER_WAVE], const int (&dma_off)[PER_WAVE]) {
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int pc = wid * PER_WAVE + i;
     const int q = q0 + dma_r[i];
-    const uint16_t* src = pc < 16 ? p.g + (int64_t)q * p.gld  // G rows >= rows are zero
-                                  : p.eps16.data + (int64_t)min(q, rows - 1) * p.eps16.ld;
+    const uint16_t* src = pc < PIECES / 2
+                              ? p.g + (int64_t)q * p.gld  // G rows >= rows are zero
+                              : p.eps16.data + (int64_t)min(q, rows - 1) * p.eps16.ld;
+    if (MPV_ABL & 128) continue;
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + dma_off[i],
                                      (__attribute__((address_space(3))) void*)(dst + pc * 1024),
                                      16, 0, 0);
@@ -276,13 +286,15 @@ MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
 }
 
 template <int WM, int WN, int TM, int TN, int kDrStages>
-__global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
+__global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
   constexpr int NW = WM * WN;
   constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
-  static_assert(BL == 128 && BZ == 128, "tile is 128 x 128 (one 512-B LDS row)");
-  constexpr int IMG = kDrKR * kDrRowB;  // 16 KB per operand
-  constexpr int STAGE = 2 * IMG;        // 32 KB
-  constexpr int PIECES = STAGE / 1024;  // 32 wave-instructions of 2 rows
+  static_assert(BL == BZ, "square tile: one LDS row layout for both operands");
+  constexpr int ROWB = BL * 4;          // bytes per LDS row: BL columns, hi + lo
+  constexpr int IMG = kDrKR * ROWB;     // per operand
+  constexpr int STAGE = 2 * IMG;
+  constexpr int PIECES = STAGE / 1024;  // 1-KB wave-instructions per stage
+  constexpr int RPP = 1024 / ROWB;      // rows per piece
   static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
   constexpr int PER_WAVE = PIECES / NW;
   constexpr int P = kDrStages - 1;
@@ -298,16 +310,19 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
   const int rows = p.B * p.S;
   const int q_begin = kc * p.rows_per_chunk;
   const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
-  // DMA lane mapping: 2 rows of 512 B per wave-instruction; per-lane byte
-  // offsets (without the stage's first row) of my PER_WAVE pieces
+  // DMA lane mapping: RPP rows per 1-KB wave-instruction; wave w moves pieces
+  // w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E rows.  Per-lane
+  // byte offsets (without the stage's first row) of my pieces:
   int dma_r[PER_WAVE], dma_off[PER_WAVE];
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int pc = wid * PER_WAVE + i;
-    dma_r[i] = ((pc & 15) << 1) + (lane >> 5);  // K row within the stage
-    const int u_lds = (lane & 31) >> 1, half = lane & 1;
+    const int pr = pc % (PIECES / 2);
+    const int lrow = lane / (64 / RPP), lpos = lane % (64 / RPP);  // 16-B slot within the row
+    dma_r[i] = pr * RPP + lrow;  // K row within the stage
+    const int u_lds = lpos >> 1, half = lpos & 1;
     const int u_src = u_lds ^ (dma_r[i] & 7);
-    dma_off[i] = 2 * 2 * (pc < 16 ? l0 : z0) + u_src * 32 + half * 16;  // chunked column start: 2*col halves
+    dma_off[i] = 4 * (pc < PIECES / 2 ? l0 : z0) + u_src * 32 + half * 16;  // chunked: 4 B/column
   }
   // transposed-read lane mapping: lane 4q+p of its 16-lane group
   const int tq = lr >> 2, tp = lr & 3;
@@ -321,40 +336,46 @@ __global__ __launch_bounds__(WM* WN * 64, 2) void dR16_kernel(Dr16Params p) {
 
   const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
   for (int j = 0; j < P && j < nst; ++j)
-    dr_issue<PER_WAVE>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_r, dma_off);
+    dr_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_r, dma_off);
   for (int ci = 0; ci < nst; ++ci) {
-    wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
+    if (P == 1)
+      wait_vmcnt<0>();
+    else
+      wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
     if (ci + P < nst)
-      dr_issue<PER_WAVE>(p, smem + ((ci + P) % kDrStages) * STAGE, q_begin + (ci + P) * kDrKR,
-                         rows, wid, dma_r, dma_off);
+      dr_issue<PER_WAVE, PIECES>(p, smem + ((ci + P) % kDrStages) * STAGE,
+                                 q_begin + (ci + P) * kDrKR, rows, wid, dma_r, dma_off);
     const char* base = smem + (ci % kDrStages) * STAGE;
     s16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
     for (int m = 0; m < TM; ++m) {
       const int t = wm * TM + m, uh = (t >> 1) * 4 + (t & 1);
       const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
-      ah[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + ch),
-                                      tr_read(base, r1 * kDrRowB + ch), 0, 1, 2, 3, 4, 5, 6, 7);
-      al[m] = __builtin_shufflevector(tr_read(base, r0 * kDrRowB + cl),
-                                      tr_read(base, r1 * kDrRowB + cl), 0, 1, 2, 3, 4, 5, 6, 7);
+      ah[m] = __builtin_shufflevector(tr_read(base, r0 * ROWB + ch),
+                                      tr_read(base, r1 * ROWB + ch), 0, 1, 2, 3, 4, 5, 6, 7);
+      al[m] = __builtin_shufflevector(tr_read(base, r0 * ROWB + cl),
+                                      tr_read(base, r1 * ROWB + cl), 0, 1, 2, 3, 4, 5, 6, 7);
     }
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
       const int t = wn * TN + n, uh = (t >> 1) * 4 + (t & 1);
       const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
-      bh[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * kDrRowB + ch),
-                                      tr_read(base + IMG, r1 * kDrRowB + ch), 0, 1, 2, 3, 4, 5, 6,
-                                      7);
-      bl[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * kDrRowB + cl),
-                                      tr_read(base + IMG, r1 * kDrRowB + cl), 0, 1, 2, 3, 4, 5, 6,
-                                      7);
+      bh[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * ROWB + ch),
+                                      tr_read(base + IMG, r1 * ROWB + ch), 0, 1, 2, 3, 4, 5, 6, 7);
+      bl[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * ROWB + cl),
+                                      tr_read(base + IMG, r1 * ROWB + cl), 0, 1, 2, 3, 4, 5, 6, 7);
     }
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
+        if (MPV_ABL & 512) {
+          acc[m][n][0] += __builtin_bit_cast(float, __builtin_shufflevector(ah[m], bl[n], 0, 8)) +
+                          __builtin_bit_cast(float, __builtin_shufflevector(al[m], bh[n], 0, 8));
+          continue;
+        }
         acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
                                                            acc[m][n], 0, 0, 0);
         acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
@@ -535,11 +556,26 @@ struct BwdPlan {
   size_t coef_bytes, colpart_bytes, slab_bytes, bound_bytes, planes_bytes;
 };
 
+constexpr int kDr16Tile = 256;  // 3xf16 dR tile: 256 x 256, 8 waves of 128 x 64
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   BwdPlan pl;
   const int64_t L = s->L, S = s->S_local, B = s->B, z = s->z;
   const bool planes = gemm == MPV_GEMM_F16X3;
-  pl.ldg = cdiv(L, 128) * 128;
+  const int64_t dr_tile = planes ? kDr16Tile : 128;  // dR output tile edge
+  pl.ldg = cdiv(L, dr_tile) * dr_tile;
   const int64_t Lc = planes ? pl.ldg : L;  // columns the element pass covers
   pl.nLc = (int)cdiv(Lc, 1024);
   pl.TPR = (int)(Lc >= 1024 ? 256 : cdiv(Lc, 4));
@@ -550,13 +586,15 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   if (want > max_chunks) want = max_chunks;
   pl.rows_per_chunk = (int)cdiv(S, want);
   pl.nSc = (int)cdiv(S, pl.rows_per_chunk);
-  pl.nLt = (int)cdiv(L, 128);
-  pl.nZt = (int)cdiv(z, 128);
+  pl.nLt = (int)cdiv(L, dr_tile);
+  pl.nZt = (int)cdiv(z, dr_tile);
   const int64_t rows = B * S;
   const int64_t tiles = (int64_t)pl.nLt * pl.nZt;
   const int64_t kr = 32;  // K rows per stage of either GEMM
   pl.rows_pad = (int)(cdiv(rows, kr) * kr);
-  int64_t kc = cdiv(1536, tiles);
+  // split-K chunks: the 3xf16 kernel (1 workgroup per CU) gets one workgroup
+  // per CU in a single wave of equal chunks; the fp32 kernel several per CU
+  int64_t kc = planes ? cdiv(num_cus(), tiles) : cdiv(1536, tiles);
   const int64_t kc_max = cdiv(rows, 256);
   if (kc > kc_max) kc = kc_max;
   if (kc < 1) kc = 1;
@@ -594,10 +632,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   if (a->dR32) {
     if (planes) {
       MPV_REQUIRE(a->eps16.data && a->eps16.scale, "eps16 planes are NULL");
-      MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * 128 && a->eps16.ld % 64 == 0 &&
+      MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * kDr16Tile && a->eps16.ld % 64 == 0 &&
                       a->eps16.rows_pad >= shape->S_local * shape->B,
                   "eps16 planes too small (ld %lld < %lld)", (long long)a->eps16.ld,
-                  2 * (long long)pl.nZt * 128);
+                  2 * (long long)pl.nZt * kDr16Tile);
     } else {
       MPV_REQUIRE(a->eps != nullptr, "MPV_GEMM_F32 needs eps");
     }
@@ -685,8 +723,9 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.nKc = pl.nKc;
       dp.rows_per_chunk = pl.dr_rows_per_chunk;
       dp.rows_pad = pl.rows_pad;
-      // 4 waves of 64 x 64, 2-stage ring (64 KB LDS): 2 workgroups per CU
-      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 4, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+      // 256 x 256 tile, 8 waves of 128 x 64, 2-stage ring (128 KB LDS)
+      static_assert(kDr16Tile == 256, "launch config below");
+      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 8, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
     } else {
       DrParams dp;
       dp.G = a->T;

@@ -54,6 +54,7 @@ class Planes:
 
 
 GEMMS = {"f16x3": H.GEMM_F16X3, "f32": H.GEMM_F32}
+EPS_PAD = 256  # noise plane columns: a whole number of 256-wide dR tiles (probit_bwd.hip)
 
 
 class HipShardBackend:
@@ -73,7 +74,7 @@ class HipShardBackend:
     def make_noise(self, shape, device, seed, offset):
         lib, st = H.load_library(), H.stream_of(device)
         if self.gemm == H.GEMM_F16X3:
-            eps = Planes(shape.S_local * shape.B, _pad(shape.z, 128), device)
+            eps = Planes(shape.S_local * shape.B, _pad(shape.z, EPS_PAD), device)
             H.check(lib.mpv_noise_philox_f16(shape, seed, offset, eps.c(), st),
                     "mpv_noise_philox_f16")
             return eps
@@ -96,7 +97,7 @@ class HipShardBackend:
         rows = shape.S_local * shape.B
         # plane rows are b-major (row b*S + s): split the (B, S, z) transpose
         eps_bs = eps.transpose(0, 1).contiguous()
-        return self._split(eps_bs, rows, shape.z, Planes(rows, _pad(shape.z, 128), eps.device))
+        return self._split(eps_bs, rows, shape.z, Planes(rows, _pad(shape.z, EPS_PAD), eps.device))
 
     def prepare_R(self, R):
         """r_sqrt_sigma (L,z) fp64/fp32 -> the GEMM operand (R.T.float(), mpvae.py:165)."""

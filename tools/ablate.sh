@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing ablations of the forward GEMM kernel: builds libmpvae_hip.so variants
+# Timing ablations of the GEMM kernels (MPV_ABL bits in probit_fwd.hip / probit_bwd.hip): builds libmpvae_hip.so variants
 # with -DMPV_ABL=<bits> (see probit_fwd.hip) into abl/<bits>/ (build here),
 # or times them on the GPU box (run).
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -9,13 +9,16 @@ case "$1" in
     cd "$R/mpvae-1_amd" && make -s >/dev/null || exit 1
     for a in $VARIANTS; do
       mkdir -p "$R/abl/$a"
-      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -Icsrc \
-        -DMPV_ABL=$a -c csrc/probit_fwd.hip -o "$R/abl/$a/probit_fwd.o" &
+      for f in probit_fwd probit_bwd; do
+        /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -Icsrc \
+          -DMPV_ABL=$a -c csrc/$f.hip -o "$R/abl/$a/$f.o" &
+      done
     done
     wait
     for a in $VARIANTS; do
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined \
-        -o "$R/abl/$a/libmpvae_hip.so" "$R/abl/$a/probit_fwd.o" build/probit_bwd.o build/util.o || exit 1
+        -o "$R/abl/$a/libmpvae_hip.so" "$R/abl/$a/probit_fwd.o" "$R/abl/$a/probit_bwd.o" \
+        build/util.o || exit 1
     done ;;
   run)
     mkdir -p "$R/gpurun_out/abl"
