@@ -113,12 +113,13 @@ def roofline(times, S_local, B, L, z, steps, gemm):
         frac = achieved / pk
     else:
         bound, achieved, pk, unit, frac = "unknown", None, None, None, None
-    breakdown = {k: round(v[1] / v[0], 4) for k, v in sorted(times.items(),
-                                                                 key=lambda kv: -kv[1][1])}
+    # milliseconds per step of every timed op (an op may be several launches)
+    breakdown = {k: round(v[1] / steps, 4) for k, v in sorted(times.items(),
+                                                              key=lambda kv: -kv[1][1])}
     return {"kernel": dom, "bound": bound, "achieved": achieved, "peak": pk, "unit": unit,
             "frac": frac, "traffic": None, "peak_basis": peak_note if bound == "mfma" else
             "HBM3E spec", "avg_ms": round(avg_s * 1e3, 4),
-            "per_launch_ms": breakdown}
+            "ms_per_step_by_op": breakdown}
 
 
 def pmc_traffic(config, kernel):

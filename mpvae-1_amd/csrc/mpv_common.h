@@ -192,8 +192,10 @@ struct u32x4 { uint32_t x, y, z, w; };
 MPV_DEV u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    // one v_mad_u64_u32 per product (lo and hi words together)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -201,15 +203,15 @@ MPV_DEV u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// Box-Muller on one word pair (see oracle/philox.py for the exact map).
+// Box-Muller on one word pair (see oracle/philox.py for the exact map), on the
+// hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 /
+// v_cos_f32, which take their argument in revolutions -- exactly v in [0, 1).
 MPV_DEV void box_muller(uint32_t we, uint32_t wo, float& n0, float& n1) {
   const float u = ((float)(we >> 8) + 0.5f) * 5.9604644775390625e-8f;   // 2^-24
   const float v = (float)(wo >> 8) * 5.9604644775390625e-8f;
-  const float r = sqrtf(-2.0f * logf(u));
-  float s, c;
-  sincospif(2.0f * v, &s, &c);
-  n0 = r * c;
-  n1 = r * s;
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u));  // -2 ln 2
+  n0 = r * __builtin_amdgcn_cosf(v);
+  n1 = r * __builtin_amdgcn_sinf(v);
 }
 
 }  // namespace mpv

@@ -262,43 +262,53 @@ __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int
 // the constant 2^12 (max |n| * s < 24200 < 65504).
 constexpr float kNoiseScale = 4096.0f;
 
-__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int64_t S,
-                                                            int64_t B, int64_t z, int64_t s_off,
-                                                            uint32_t k0, uint32_t k1,
-                                                            uint64_t offset) {
-  const int64_t q4 = out.ld >> 3;  // 4-column groups per row
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= S * B * q4) return;
-  const int64_t r = i / q4, c0 = (i - r * q4) * 4;
-  const int64_t bb = r / S, ss = r - bb * S;
-  const int64_t e_row = (s_off + ss) * B + bb;  // row of the global (S_total, B, z) draw
-  uint64_t cached = ~0ull;
-  u32x4 w = {0u, 0u, 0u, 0u};
-  uint16_t h[4], l[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t c = c0 + q;
-    float v = 0.0f;
-    if (c < z) {
-      const int64_t e = e_row * z + c;  // global element index
-      const uint64_t g = (uint64_t)(e >> 2);
-      if (g != cached) {
-        const uint64_t ctr = g + offset;
-        w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
-        cached = g;
+// One block per plane row r = b*S + s; a thread makes 4 consecutive columns.
+// With z % 4 == 0 those are the 4 words of ONE Philox call (2 Box-Muller
+// pairs); otherwise each column picks its word from the call covering it.
+__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
+                                                            int z, int64_t s_off, uint32_t k0,
+                                                            uint32_t k1, uint64_t offset) {
+  const int r = blockIdx.x;
+  const int bb = r / S, ss = r - bb * S;
+  const int64_t e_row = ((s_off + ss) * B + bb) * (int64_t)z;  // first global element of the row
+  const int cols = (int)(out.ld >> 1);
+  for (int c0 = threadIdx.x * 4; c0 < cols; c0 += blockDim.x * 4) {
+    float v[4];
+    if ((z & 3) == 0) {
+      if (c0 < z) {
+        const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
+        const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+        box_muller(w.x, w.y, v[0], v[1]);
+        box_muller(w.z, w.w, v[2], v[3]);
+      } else {
+        v[0] = v[1] = v[2] = v[3] = 0.0f;
       }
-      float n0, n1;
-      const int ln = (int)(e & 3);
-      if (ln < 2) box_muller(w.x, w.y, n0, n1);
-      else box_muller(w.z, w.w, n0, n1);
-      v = (ln & 1) ? n1 : n0;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + q;
+        v[q] = 0.0f;
+        if (c < z) {
+          const int64_t e = e_row + c;
+          const uint64_t ctr = (uint64_t)(e >> 2) + offset;
+          const u32x4 w =
+              philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+          float n0, n1;
+          const int ln = (int)(e & 3);
+          if (ln < 2) box_muller(w.x, w.y, n0, n1);
+          else box_muller(w.z, w.w, n0, n1);
+          v[q] = (ln & 1) ? n1 : n0;
+        }
+      }
     }
-    split_f16(v, kNoiseScale, h[q], l[q]);
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_f16(v[q], kNoiseScale, h[q], l[q]);
+    const int64_t o = chunked_index(r, out.ld, c0);
+    *reinterpret_cast<s16x4*>(out.data + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+    *reinterpret_cast<s16x4*>(out.data + o + kLoOff) =
+        s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
   }
-  const int64_t o = chunked_index(r, out.ld, c0);
-  *reinterpret_cast<s16x4*>(out.data + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-  *reinterpret_cast<s16x4*>(out.data + o + kLoOff) =
-      s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
 }
 
 __global__ void set_scalar_kernel(float* p, float v) { *p = v; }
@@ -417,12 +427,12 @@ int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
   const int64_t rows = shape->S_local * shape->B;
   MPV_REQUIRE(out->rows_pad >= rows && out->ld / 2 >= shape->z, "noise planes too small");
   hipStream_t s = as_stream(stream);
-  MPV_LAUNCH("noise_philox", set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
-  const int64_t n = rows * (out->ld / 8);
-  MPV_REQUIRE(cdiv(n, 256) < (int64_t(1) << 31), "noise too large");
-  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
-             *out, shape->S_local, shape->B, shape->z, shape->s_offset, (uint32_t)seed,
-             (uint32_t)(seed >> 32), offset);
+  hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
+  MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
+  const unsigned threads = out->ld / 8 >= 256 ? 256 : (unsigned)(cdiv(out->ld / 8, 64) * 64);
+  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)rows), dim3(threads), 0, s,
+             *out, (int)shape->S_local, (int)shape->B, (int)shape->z, shape->s_offset,
+             (uint32_t)seed, (uint32_t)(seed >> 32), offset);
   return check_launch("noise_philox_f16");
 }
 

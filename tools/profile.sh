@@ -8,7 +8,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${TAG:-c4}"
 ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}"
 OUT="$R/gpurun_out/prof/$TAG"
-KRE="${KRE:-probit_fwd|dR_gemm|bwd_elem|noise_philox}"
+KRE="${KRE:-probit_fwd|dR16|dR_gemm|bwd_elem|noise_philox}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 run() {  # name, rocprof args...
