@@ -71,6 +71,43 @@ MPV_DEV float probit_prob(float u) {
   return probit_eval(u, phi);
 }
 
+// ---- packed fp32 (v_pk_fma/mul/add_f32: two lanes' worth per issue) -------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+MPV_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+MPV_DEV f32x2 splat2(float v) { return f32x2{v, v}; }
+
+// probit_eval of the label and feature branches at once (every step is the
+// same for both), bit-identical to two probit_eval calls: the fused steps are
+// explicit fmas and the reference-order steps stay separately rounded.
+MPV_DEV f32x2 probit_eval2(f32x2 u, f32x2& phi) {
+#pragma clang fp contract(off)
+  const f32x2 z = f32x2{fabsf(u.x), fabsf(u.y)} * kInvSqrt2;
+  const f32x2 den = pk_fma(splat2(0.5f), z, splat2(1.0f));
+  const f32x2 t = f32x2{fast_rcp(den.x), fast_rcp(den.y)};
+  f32x2 p = pk_fma(t, splat2(0.17087277f), splat2(-0.82215223f));
+  p = pk_fma(t, p, splat2(1.48851587f));
+  p = pk_fma(t, p, splat2(-1.13520398f));
+  p = pk_fma(t, p, splat2(0.27886807f));
+  p = pk_fma(t, p, splat2(-0.18628806f));
+  p = pk_fma(t, p, splat2(0.09678418f));
+  p = pk_fma(t, p, splat2(0.37409196f));
+  p = pk_fma(t, p, splat2(1.00002368f));
+  p = pk_fma(t, p, splat2(-1.26551223f));
+  // fast_exp(x) = exp2(x * log2 e), as in probit_eval
+  const f32x2 az = (-z * z) * 1.4426950408889634f;
+  const f32x2 ap = p * 1.4426950408889634f;
+  const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
+  const f32x2 ep = f32x2{__builtin_amdgcn_exp2f(ap.x), __builtin_amdgcn_exp2f(ap.y)};
+  phi = ez * kInvSqrt2Pi;
+  const f32x2 erfc_z = (t * ez) * ep;
+  const f32x2 om = splat2(1.0f) - erfc_z;  // 1 - erfc, rounded once
+  // erf(u) = +-(1 - erfc): erfc - 1 is exactly -(1 - erfc)
+  const f32x2 erf_u = f32x2{u.x < 0.0f ? -om.x : om.x, u.y < 0.0f ? -om.y : om.y};
+  const f32x2 cdf = splat2(0.5f) * (splat2(1.0f) + erf_u);
+  return cdf * kC1 + splat2(kC0);
+}
+
 // ---- DPP row (16-lane) reductions ------------------------------------------
 // row_shr:n = 0x110 + n.  After the 4 steps lane 15 of every 16-lane row holds
 // the row's sum (bound_ctrl: lanes shifted in from outside the row read 0).

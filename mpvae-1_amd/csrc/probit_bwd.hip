@@ -102,21 +102,53 @@ struct ElemParams {
   float inv_S;
 };
 
-MPV_DEV float d_elem(float t, float base, float y, bool soft, float alpha, float bP, float bN,
-                     float gind) {
-  const float u = t + base;
-  float phi;
-  const float E = probit_eval(u, phi);
-  // d logp / dE = y/E - (1-y)/(1-E)  (mpvae.py:184-185)
-  float dl = (y == 0.0f) ? -fast_rcp(1.0f - E) : fast_rcp(E);
-  if (soft) dl = y / E - (1.0f - y) / (1.0f - E);
-  float dE = alpha * dl + gind;
+// dL/dt of one element for the label (.x) and feature (.y) branches at once
+// (packed fp32): u = t + base, E = probit(u),
+//   dE = alpha (y/E - (1-y)/(1-E)) + [y=1](-betaP) e^{-5E} + [y=0] betaN e^{5E} + g_ind
+// (mpvae.py:110-117, 184-185 differentiated), dL/dt = dE (1-1e-6) phi(u).
+MPV_DEV f32x2 d_elem2(float t, f32x2 base, float y, bool soft, f32x2 alpha, f32x2 bP, f32x2 bN,
+                      f32x2 gind) {
+  f32x2 phi;
+  const f32x2 E = probit_eval2(splat2(t) + base, phi);
+  // d logp / dE = y/E - (1-y)/(1-E): one reciprocal for a 0/1 label
+  const f32x2 q = (y == 0.0f) ? splat2(1.0f) - E : E;
+  f32x2 dl = f32x2{fast_rcp(q.x), fast_rcp(q.y)};
+  if (y == 0.0f) dl = -dl;
+  if (soft) dl = splat2(y) / E - splat2(1.0f - y) / (splat2(1.0f) - E);
+  f32x2 dE = pk_fma(alpha, dl, gind);
   // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-  const float rk = (y == 1.0f) ? -bP : ((y == 0.0f) ? bN : 0.0f);
-  dE = fmaf(rk, fast_exp((y == 1.0f ? -5.0f : 5.0f) * E), dE);
+  const f32x2 rk = (y == 1.0f) ? -bP : ((y == 0.0f) ? bN : splat2(0.0f));
+  const f32x2 a = E * (y == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+  dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
   // a degenerate row poisons every label, whatever its value (reference autograd)
-  if (bP != bP) dE = bP;
-  return dE * kC1 * phi;
+  if (bP.x != bP.x) dE.x = bP.x;
+  if (bP.y != bP.y) dE.y = bP.y;
+  return (dE * kC1) * phi;
+}
+
+// Inputs of one row s of the element pass: its six coefficients (label .x,
+// feature .y) and the lane's four t values.
+struct ElemRow {
+  f32x2 alpha, bP, bN;
+  float t[4];
+};
+
+template <bool VEC>
+MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0,
+                           const bool (&ok)[4]) {
+  const int64_t cb = (int64_t)b * p.S + s;
+  const int64_t BS = (int64_t)p.B * p.S;
+  r.alpha = f32x2{p.coef[0 * BS + cb], p.coef[3 * BS + cb]};
+  r.bP = f32x2{p.coef[1 * BS + cb], p.coef[4 * BS + cb]};
+  r.bN = f32x2{p.coef[2 * BS + cb], p.coef[5 * BS + cb]};
+  const float* row = p.T + cb * p.L;
+  if (VEC && c0 + 3 < p.L) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
+    r.t[0] = v[0]; r.t[1] = v[1]; r.t[2] = v[2]; r.t[3] = v[3];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.t[q] = ok[q] ? row[c0 + q] : 0.0f;
+  }
 }
 
 template <bool VEC, bool PLANES>
@@ -148,28 +180,21 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
   if (active && c0 < p.Lc) {
-    for (int s = s_begin + rsub; s < s_end; s += p.RPI) {
+    // one row of lookahead: row s+RPI's loads are in flight while row s computes
+    const int s0 = s_begin + rsub;
+    ElemRow cur, nxt;
+    if (s0 < s_end) elem_row_load<VEC>(cur, p, b, s0, c0, ok);
+    for (int s = s0; s < s_end; s += p.RPI) {
+      if (s + p.RPI < s_end) elem_row_load<VEC>(nxt, p, b, s + p.RPI, c0, ok);
       const int64_t cb = (int64_t)b * S + s;
-      const int64_t BS = (int64_t)B * S;
-      const float ae = p.coef[0 * BS + cb], pe = p.coef[1 * BS + cb], ne = p.coef[2 * BS + cb];
-      const float ax = p.coef[3 * BS + cb], px = p.coef[4 * BS + cb], nx = p.coef[5 * BS + cb];
-      float* row = p.T + cb * L;
-      float t[4];
-      if (VEC && c0 + 3 < L) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
-        t[0] = v[0]; t[1] = v[1]; t[2] = v[2]; t[3] = v[3];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = ok[q] ? row[c0 + q] : 0.0f;
-      }
       float G[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float ge = d_elem(t[q], fe[q], yv[q], soft[q], ae, pe, ne, gil[q]);
-        const float gx = d_elem(t[q], fx[q], yv[q], soft[q], ax, px, nx, gi[q]);
-        se[q] += ok[q] ? ge : 0.0f;
-        sx[q] += ok[q] ? gx : 0.0f;
-        G[q] = ok[q] ? ge + gx : 0.0f;
+        const f32x2 g2 = d_elem2(cur.t[q], f32x2{fe[q], fx[q]}, yv[q], soft[q], cur.alpha,
+                                 cur.bP, cur.bN, f32x2{gil[q], gi[q]});
+        se[q] += ok[q] ? g2.x : 0.0f;
+        sx[q] += ok[q] ? g2.y : 0.0f;
+        G[q] = ok[q] ? g2.x + g2.y : 0.0f;
       }
       if (PLANES) {
         uint16_t h[4], l[4];
@@ -180,13 +205,17 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
         *reinterpret_cast<s16x4*>(p.g + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
         *reinterpret_cast<s16x4*>(p.g + o + kLoOff) =
             s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
-      } else if (VEC && c0 + 3 < L) {
-        *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
       } else {
+        float* row = p.T + cb * L;
+        if (VEC && c0 + 3 < L) {
+          *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
+        } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (ok[q]) row[c0 + q] = G[q];
+          for (int q = 0; q < 4; ++q)
+            if (ok[q]) row[c0 + q] = G[q];
+        }
       }
+      cur = nxt;
     }
   }
   // column sums over this block's rows: reduce the RPI row-lanes per column
@@ -580,7 +609,8 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.nLc = (int)cdiv(Lc, 1024);
   pl.TPR = (int)(Lc >= 1024 ? 256 : cdiv(Lc, 4));
   pl.RPI = 256 / pl.TPR;
-  int64_t want = cdiv(2048, B * pl.nLc);
+  // s-chunks: enough blocks for several rounds of resident blocks (short tail)
+  int64_t want = cdiv(8192, B * pl.nLc);
   if (want < 1) want = 1;
   const int64_t max_chunks = cdiv(S, pl.RPI);
   if (want > max_chunks) want = max_chunks;

@@ -71,13 +71,13 @@ MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
 // col = lane & 15 within each 16-wide tile), and its running column sums.
 template <int TN>
 struct FwdLane {
-  float colE[TN], colEx[TN];
+  f32x2 col[TN];  // running column sums of E: label (.x) and feature (.y) branch
 };
 
 template <int WN, int TN>
 MPV_DEV void fwd_lane_init(FwdLane<TN>& ln) {
 #pragma unroll
-  for (int n = 0; n < TN; ++n) ln.colE[n] = ln.colEx[n] = 0.0f;
+  for (int n = 0; n < TN; ++n) ln.col[n] = splat2(0.0f);
 }
 
 // Label-column constants of the lane (fe_out, fx_out, y of its TN columns).
@@ -164,36 +164,35 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
       const int rl = wm * TM * 16 + m * 16 + lg * 4 + i;
       const int s = s0 + rl;
       const bool rowok = s >= s_own && s < S;
-      float st6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // row sums, label (.x) and feature (.y) branch: log-prob, P, N
+      f32x2 sl = splat2(0.0f), sp = splat2(0.0f), sn = splat2(0.0f);
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
         const bool ok = rowok && cl.colok[n];
         const float t = acc[m][n][i] * scale;
-        if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + cl.col[n]] = t;
-        const float E = probit_prob(t + cl.fe[n]);
-        const float Ex = probit_prob(t + cl.fx[n]);
+        if (!(MPV_ABL & 2) && p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + cl.col[n]] = t;
+        f32x2 phi;
+        const f32x2 E = probit_eval2(splat2(t) + f32x2{cl.fe[n], cl.fx[n]}, phi);
         const float y = cl.y[n];
         // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
-        float le = fast_log(y == 0.0f ? 1.0f - E : E);
-        float lx = fast_log(y == 0.0f ? 1.0f - Ex : Ex);
+        const f32x2 q = (y == 0.0f) ? splat2(1.0f) - E : E;
+        f32x2 lp = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)} *
+                   0.6931471805599453f;
         if (cl.soft[n]) {
-          le = y * fast_log(E) + (1.0f - y) * fast_log(1.0f - E);
-          lx = y * fast_log(Ex) + (1.0f - y) * fast_log(1.0f - Ex);
+          lp.x = y * fast_log(E.x) + (1.0f - y) * fast_log(1.0f - E.x);
+          lp.y = y * fast_log(E.y) + (1.0f - y) * fast_log(1.0f - E.y);
         }
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-        const float sg = (y == 1.0f) ? -5.0f : 5.0f;
-        const float re = fast_exp(sg * E), rx = fast_exp(sg * Ex);
+        const f32x2 a = E * ((y == 1.0f) ? -5.0f : 5.0f) * 1.4426950408889634f;
+        const f32x2 r = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
         const float wpos = (ok && y == 1.0f) ? 1.0f : 0.0f;
         const float wneg = (ok && y == 0.0f) ? 1.0f : 0.0f;
-        st6[0] += ok ? le : 0.0f;
-        st6[1] += ok ? lx : 0.0f;
-        st6[2] += wpos * re;
-        st6[3] += wneg * re;
-        st6[4] += wpos * rx;
-        st6[5] += wneg * rx;
-        ln.colE[n] += rowok ? E : 0.0f;
-        ln.colEx[n] += rowok ? Ex : 0.0f;
+        sl += ok ? lp : splat2(0.0f);
+        sp = pk_fma(splat2(wpos), r, sp);
+        sn = pk_fma(splat2(wneg), r, sn);
+        ln.col[n] += rowok ? E : splat2(0.0f);
       }
+      float st6[6] = {sl.x, sl.y, sp.x, sn.x, sp.y, sn.y};
 #pragma unroll
       for (int k = 0; k < 6; ++k) st6[k] = row16_sum_to_lane15(st6[k]);
       if (lr == 15) {
@@ -230,7 +229,7 @@ MPV_DEV void fwd_colsum_epilogue(const FwdParams& p, FwdLane<TN>& ln, int b, int
   float* cred = smem;  // [WM][BN][2]
 #pragma unroll
   for (int n = 0; n < TN; ++n) {
-    float e = ln.colE[n], x = ln.colEx[n];
+    float e = ln.col[n].x, x = ln.col[n].y;
     e += __shfl_xor(e, 16, 64);
     e += __shfl_xor(e, 32, 64);
     x += __shfl_xor(x, 16, 64);
