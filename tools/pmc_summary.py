@@ -34,6 +34,18 @@ def counters(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+# in-library timing tag (bench.py roofline "kernel") -> kernel name prefix
+TAGS = {"probit_fwd": "probit_fwd", "dR_gemm": ("dR16", "dR_gemm"), "bwd_elem": "bwd_elem",
+        "noise_philox": "noise_philox"}
+
+
+def tag_of(kernel):
+    for t, pre in TAGS.items():
+        if kernel.startswith(pre):
+            return t
+    return None
+
+
 def main(src, dst, tag):
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "trace_kernel_stats.csv")
@@ -57,6 +69,11 @@ def main(src, dst, tag):
                              "avg_ms_trace": dur.get(k, (None, None))[1],
                              "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                              "hbm_bytes_per_launch": hbm}
+    # aliases under the timing tags bench.py reports (e.g. probit_fwd16 -> probit_fwd)
+    for k in list(out["kernels"]):
+        t = tag_of(k)
+        if t is not None and t not in out["kernels"]:
+            out["kernels"][t] = dict(out["kernels"][k], kernel=k)
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
