@@ -205,6 +205,28 @@ MPV_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS address (byte offset in the workgroup's LDS) of a __shared__ pointer.
+MPV_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// LDS-DMA of 16 B per lane (global_load_lds_dwordx4, saddr form): lane i's 16 B
+// at saddr + voff land at LDS byte lds + 16*i.  Issued through inline asm so
+// that hipcc's waitcnt pass does not see an LDS store: it otherwise puts an
+// s_waitcnt vmcnt(0) before every later ds_read (it cannot tell the stage
+// images of a ring apart), which exposes the whole DMA latency at every stage.
+// Callers order it themselves: counted s_waitcnt vmcnt + a barrier before a
+// stage is read, and a barrier after its last read before it is refilled.
+MPV_DEV void lds_dma16(const void* saddr, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(saddr), "s"(lds)
+      : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n (the immediate must be a constant).
 MPV_DEV void wait_vmcnt_dyn(int n) {
 #define MPV_VMC(k) \

@@ -268,6 +268,26 @@ struct Dr16Params {
 #ifndef MPV_ABL
 #define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
 #endif
+// In-kernel phase stamps (timing studies only, MPV_ABL & 1024): s_memtime at
+// the loop's phase points of blocks 0-1, iterations 256..287, every wave.
+#if (MPV_ABL & 1024)
+__device__ unsigned long long g_dr_stamps[2][8][32][4];
+#define MPV_STAMP(k)                                                                     \
+  do {                                                                                   \
+    if (blockIdx.x < 2 && ci >= 256 && ci < 288 && (threadIdx.x & 63) == 0)              \
+      g_dr_stamps[blockIdx.x][threadIdx.x >> 6][ci - 256][k] = __builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define MPV_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+#ifndef MPV_DR_KIND
+#define MPV_DR_KIND 0  // 0: 16x16x32 ring, 1: 16x16x32 staggered, 2: 32x32x16 4-deep ring
+#endif
+#ifndef MPV_DMA_ASM
+#define MPV_DMA_ASM 1
+#endif
 
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 
@@ -308,9 +328,12 @@ MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
                               ? p.g + (int64_t)q * p.gld  // G rows >= rows are zero
                               : p.eps16.data + (int64_t)min(q, rows - 1) * p.eps16.ld;
     if (MPV_ABL & 128) continue;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + dma_off[i],
-                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
-                                     16, 0, 0);
+    if (MPV_DMA_ASM)
+      lds_dma16(src, (uint32_t)dma_off[i], lds_addr(dst + pc * 1024));
+    else
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + dma_off[i],
+                                       (__attribute__((address_space(3))) void*)(dst + pc * 1024),
+                                       16, 0, 0);
   }
 }
 
@@ -367,15 +390,19 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
   for (int j = 0; j < P && j < nst; ++j)
     dr_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_r, dma_off);
   for (int ci = 0; ci < nst; ++ci) {
+    MPV_STAMP(0);
     if (P == 1)
       wait_vmcnt<0>();
     else
       wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    MPV_STAMP(1);
     barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
+    MPV_STAMP(2);
     if (ci + P < nst)
       dr_issue<PER_WAVE, PIECES>(p, smem + ((ci + P) % kDrStages) * STAGE,
                                  q_begin + (ci + P) * kDrKR, rows, wid, dma_r, dma_off);
+    MPV_STAMP(3);
     const char* base = smem + (ci % kDrStages) * STAGE;
     s16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
@@ -424,6 +451,307 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
         const int l = l0 + (wm * TM + m) * 16 + lg * 4 + i;
         const int zc = z0 + (wn * TN + n) * 16 + lr;
         if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][i] * inv;
+      }
+}
+
+// Fragments of one dR stage (per wave: TM A tiles and TN B tiles, hi and lo).
+template <int TM, int TN>
+struct DrFrag {
+  s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+};
+
+template <int TM, int TN, int ROWB, int IMG>
+MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0, int r1, int sw,
+                     int tp) {
+#pragma unroll
+  for (int m = 0; m < TM; ++m) {
+    const int t = wm * TM + m, uh = (t >> 1) * 4 + (t & 1);
+    const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
+    f.ah[m] = __builtin_shufflevector(tr_read(base, r0 * ROWB + ch), tr_read(base, r1 * ROWB + ch),
+                                      0, 1, 2, 3, 4, 5, 6, 7);
+    f.al[m] = __builtin_shufflevector(tr_read(base, r0 * ROWB + cl), tr_read(base, r1 * ROWB + cl),
+                                      0, 1, 2, 3, 4, 5, 6, 7);
+  }
+#pragma unroll
+  for (int n = 0; n < TN; ++n) {
+    const int t = wn * TN + n, uh = (t >> 1) * 4 + (t & 1);
+    const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
+    f.bh[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * ROWB + ch),
+                                      tr_read(base + IMG, r1 * ROWB + ch), 0, 1, 2, 3, 4, 5, 6, 7);
+    f.bl[n] = __builtin_shufflevector(tr_read(base + IMG, r0 * ROWB + cl),
+                                      tr_read(base + IMG, r1 * ROWB + cl), 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+template <int TM, int TN>
+MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
+                                                         acc[m][n], 0, 0, 0);
+    }
+}
+
+// One stage's LDS-DMA for wave wn of group 0: pieces wn*PER_WAVE .. (one row
+// each: the first PIECES/2 are G rows, the rest E rows).
+template <int PER_WAVE, int PIECES>
+MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn, int l0, int z0,
+                       int lane_u, int lane_h) {
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int pc = wn * PER_WAVE + i;  // wave-uniform
+    const bool is_g = pc < PIECES / 2;
+    const int r = is_g ? pc : pc - PIECES / 2;
+    const int q = q0 + r;
+    const char* src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
+                           : reinterpret_cast<const char*>(p.eps16.data +
+                                                           (int64_t)min(q, rows - 1) * p.eps16.ld +
+                                                           2 * z0);
+    if (MPV_ABL & 128) continue;
+    __builtin_amdgcn_global_load_lds(src + ((lane_u ^ (r & 7)) << 5) + lane_h,
+                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// Staggered schedule: the waves of row wm = 0 (group 0) and wm = 1 (group 1)
+// share the SIMDs pairwise and run one phase apart, so on every SIMD one wave
+// issues MFMAs while the other streams/reads.  Time is cut into slots ended by
+// one barrier each; group 0 does mem(i) in slot 2i and mma(i) in slot 2i+1,
+// group 1 does mem(i) in slot 2i+1 and mma(i) in slot 2i+2.
+//   mem(i): [group 0 only: LDS-DMA stage i+1 into image (i+1)%2 -- read by
+//           group 1 in slot 2i-1, so free] + fragment reads of stage i.
+//   mma(i): 96 MFMAs; group 0 then waits for its stage i+1 DMA, so stage i+1
+//           is visible to both groups after the slot's barrier.
+// Two 64-KB stage images; DMA latency budget = one slot pair.
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
+  static_assert(WM == 2, "two wave groups");
+  constexpr int NW = WM * WN;
+  constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
+  static_assert(BL == BZ, "square tile: one LDS row layout for both operands");
+  constexpr int ROWB = BL * 4;          // bytes per LDS row: BL columns, hi + lo
+  constexpr int IMG = kDrKR * ROWB;     // per operand
+  constexpr int STAGE = 2 * IMG;
+  constexpr int PIECES = STAGE / 1024;  // 1-KB wave-instructions per stage
+  constexpr int RPP = 1024 / ROWB;      // rows per piece
+  constexpr int PER_WAVE = PIECES / WN; // group 0 streams everything
+  static_assert(PIECES % WN == 0, "DMA pieces must split over group 0");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  int kc, tile;
+  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
+  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int grp = wm;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int rows = p.B * p.S;
+  const int q_begin = kc * p.rows_per_chunk;
+  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
+  static_assert(RPP == 1, "one 1-KB row per DMA piece");
+  // per-lane part of a piece's source offset: 16-B slot `lane` of the row
+  // (32-B unit lane/2, swizzled by the row's r & 7, which cycles with the piece)
+  const int lane_u = lane >> 1, lane_h = (lane & 1) * 16;
+  const int tq = lr >> 2, tp = lr & 3;
+  const int r0 = lg * 4 + tq, r1 = r0 + 16, sw = r0 & 7;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
+  if (grp == 0 && nst > 0) {
+    drs_issue<PER_WAVE, PIECES>(p, smem, q_begin, rows, wn, l0, z0, lane_u, lane_h);
+    wait_vmcnt<0>();
+  }
+  barrier_raw();
+  DrFrag<TM, TN> f;
+  // the two groups run the same number of barriers: 2*nst + 1
+  if (grp == 0) {
+    for (int i = 0; i < nst; ++i) {
+      // slot 2i: stream stage i+1, read stage i
+      if (i + 1 < nst)
+        drs_issue<PER_WAVE, PIECES>(p, smem + ((i + 1) & 1) * STAGE, q_begin + (i + 1) * kDrKR,
+                                    rows, wn, l0, z0, lane_u, lane_h);
+      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
+      lds_barrier();
+      // slot 2i+1: MFMAs of stage i; stage i+1 landed before the barrier
+      __builtin_amdgcn_s_setprio(1);
+      dr_mfma<TM, TN>(acc, f);
+      __builtin_amdgcn_s_setprio(0);
+      wait_vmcnt<0>();
+      barrier_raw();
+    }
+    barrier_raw();
+  } else {
+    barrier_raw();
+    for (int i = 0; i < nst; ++i) {
+      // slot 2i+1: read stage i
+      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
+      lds_barrier();
+      // slot 2i+2: MFMAs of stage i
+      __builtin_amdgcn_s_setprio(1);
+      dr_mfma<TM, TN>(acc, f);
+      __builtin_amdgcn_s_setprio(0);
+      barrier_raw();
+    }
+  }
+  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int l = l0 + (wm * TM + m) * 16 + lg * 4 + i;
+        const int zc = z0 + (wn * TN + n) * 16 + lr;
+        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][i] * inv;
+      }
+}
+
+// ---- dR on v_mfma_f32_32x32x16_f16: 16-row stages, 4-deep ring -------------
+// K = 16 per MFMA, so a stage of 16 sample rows (32 KB for a 256 x 256 tile)
+// is consumed on its own and the 128-KB ring keeps 3 stages in flight (the
+// 16x16x32 kernel above, at 32 rows per stage, fits one).  Fragment of a
+// 32-column block for lane l: column l%32, K rows 8*(l/32) .. +7, as two
+// transposed reads (rows 8*(l/32) + 4h + 0..3); A and B share that K order, so
+// it is the identity.  Image rows are 1 KB (256 columns chunked hi/lo); the
+// 32-B unit U of row r sits at U ^ ((r & 3) << 1), conflict-free for these
+// reads (checked exhaustively).
+constexpr int kDr32KR = 16;  // K rows per stage
+constexpr int kDr32NS = 4;   // ring depth
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+MPV_DEV int dr32_swz(int r) { return (r & 3) << 1; }
+
+template <int PER_WAVE, int PIECES>
+MPV_DEV void dr32_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid, int l0, int z0,
+                        int lane_u, int lane_h) {
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int pc = wid * PER_WAVE + i;  // wave-uniform
+    const bool is_g = pc < PIECES / 2;
+    const int r = is_g ? pc : pc - PIECES / 2;
+    const int q = q0 + r;
+    const char* src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
+                           : reinterpret_cast<const char*>(p.eps16.data +
+                                                           (int64_t)min(q, rows - 1) * p.eps16.ld +
+                                                           2 * z0);
+    if (MPV_ABL & 128) continue;
+    __builtin_amdgcn_global_load_lds(src + ((lane_u ^ dr32_swz(r)) << 5) + lane_h,
+                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <int TM, int TN>
+struct Dr32Frag {
+  s16x8 ah[TM], al[TM], bh[TN], bl[TN];
+};
+
+// tile t = 32-column block index within the 256-column image
+template <int ROWB>
+MPV_DEV s16x8 dr32_frag(const char* img, int t, int plane, int lg, int tq, int tp) {
+  const int slice = 2 * t + (lg & 1);
+  const int U = (slice >> 1) * 4 + (slice & 1) + plane;
+  const int rA = 8 * (lg >> 1) + tq, rB = rA + 4;
+  return __builtin_shufflevector(tr_read(img, rA * ROWB + ((U ^ dr32_swz(rA)) << 5) + tp * 8),
+                                 tr_read(img, rB * ROWB + ((U ^ dr32_swz(rB)) << 5) + tp * 8), 0,
+                                 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(WM* WN * 64, 1) void dR32_kernel(Dr16Params p) {
+  constexpr int NW = WM * WN;
+  constexpr int BL = WM * TM * 32, BZ = WN * TN * 32;
+  static_assert(BL == 256 && BZ == 256, "256 x 256 tile");
+  constexpr int ROWB = BL * 4;
+  constexpr int IMG = kDr32KR * ROWB;   // 16 KB per operand
+  constexpr int STAGE = 2 * IMG;        // 32 KB
+  constexpr int PIECES = STAGE / 1024;  // 32 rows of 1 KB
+  static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
+  constexpr int PER_WAVE = PIECES / NW;
+  constexpr int P = kDr32NS - 1;        // stages in flight
+  __shared__ __attribute__((aligned(1024))) char smem[kDr32NS * STAGE];
+
+  int kc, tile;
+  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
+  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tq = lr >> 2, tp = lr & 3;
+  const int rows = p.B * p.S;
+  const int q_begin = kc * p.rows_per_chunk;
+  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
+  const int lane_u = lane >> 1, lane_h = (lane & 1) * 16;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[m][n][j] = 0.0f;
+
+  const int nst = (q_end - q_begin + kDr32KR - 1) / kDr32KR;
+  for (int j = 0; j < P && j < nst; ++j)
+    dr32_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDr32KR, rows, wid, l0, z0,
+                                 lane_u, lane_h);
+  for (int ci = 0; ci < nst; ++ci) {
+    wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
+    if (ci + P < nst)
+      dr32_issue<PER_WAVE, PIECES>(p, smem + ((ci + P) % kDr32NS) * STAGE,
+                                   q_begin + (ci + P) * kDr32KR, rows, wid, l0, z0, lane_u,
+                                   lane_h);
+    const char* base = smem + (ci % kDr32NS) * STAGE;
+    Dr32Frag<TM, TN> f;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      f.ah[m] = dr32_frag<ROWB>(base, wm * TM + m, 0, lg, tq, tp);
+      f.al[m] = dr32_frag<ROWB>(base, wm * TM + m, 2, lg, tq, tp);
+    }
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      f.bh[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 0, lg, tq, tp);
+      f.bl[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 2, lg, tq, tp);
+    }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+      }
+  }
+  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
+  // D[i = l][j = z], 32x32 block: reg j -> row 8*(j/4) + 4*(lane/32) + j%4, col lane%32
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int l = l0 + (wm * TM + m) * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+        const int zc = z0 + (wn * TN + n) * 32 + (lane & 31);
+        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][j] * inv;
       }
 }
 
@@ -644,6 +972,13 @@ using namespace mpv;
 
 extern "C" {
 
+#if (MPV_ABL & 1024)
+int mpv_dbg_dr_stamps(void* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dr_stamps), sizeof(g_dr_stamps)) == hipSuccess
+             ? 0 : 1;
+}
+#endif
+
 size_t mpv_bwd_workspace_bytes(const mpv_shape* shape, int gemm) {
   if (check_shape(shape) != MPV_OK) return 0;
   const BwdPlan pl = plan_bwd(shape, gemm);
@@ -755,7 +1090,12 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.rows_pad = pl.rows_pad;
       // 256 x 256 tile, 8 waves of 128 x 64, 2-stage ring (128 KB LDS)
       static_assert(kDr16Tile == 256, "launch config below");
-      MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 8, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+      if (MPV_DR_KIND == 2)
+        MPV_LAUNCH("dR_gemm", (dR32_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+      else if (MPV_DR_KIND == 1)
+        MPV_LAUNCH("dR_gemm", (dR16s_kernel<2, 4, 8, 4>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+      else
+        MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 8, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
     } else {
       DrParams dp;
       dp.G = a->T;

@@ -459,9 +459,10 @@ struct Fwd16Dma {
     return (GA - wid + NW - 1) / NW + (GB - wid + NW - 1) / NW;
   }
 
-  MPV_DEV static void piece(const char* src, char* dst) {
+  // base: wave-uniform (SGPRs); off: per-lane byte offset (inline-asm DMA, see lds_dma16)
+  MPV_DEV static void piece(const char* base, uint32_t off, char* dst) {
     if (MPV_ABL & 4) return;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    lds_dma16(base, off, lds_addr(dst));
   }
 
   // Stream the next stage (if any) into stage image `dst`.
@@ -471,12 +472,12 @@ struct Fwd16Dma {
 #pragma unroll
     for (int j = 0; j < JA; ++j) {
       const int pc = wid + j * NW;
-      if (GA % NW == 0 || pc < GA) piece(a_base + kb + offa[j], dst + pc * 1024);
+      if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[j], dst + pc * 1024);
     }
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
       const int pc = wid + j * NW;
-      if (GB % NW == 0 || pc < GB) piece(b_base + kb + offb[j], dst + BM * kRowB + pc * 1024);
+      if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
     }
     ++issued;
     if (++kc == nK) {

@@ -1,0 +1,42 @@
+"""Read the dR16 in-kernel phase stamps of an MPV_ABL&1024 build (timing study).
+
+    MPVAE_HIP_LIB=abl/<variant>/libmpvae_hip.so python tools/stamps.py
+Runs two C4 steps through bench.py's step(), then prints per-phase cycle
+counts (median over iterations 256..287 of blocks 0-1) for every wave.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
+import torch  # noqa: E402
+import bench  # noqa: E402
+import mpvae_hip as H  # noqa: E402
+
+dev = torch.device("cuda", 0)
+L, z, B, S, d, nllc, cc, _ = bench.CONFIGS["c4"]
+args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S, mode="train",
+                          nll_coeff=nllc, c_coeff=cc, mpvae_noise="philox", mpvae_shard=False,
+                          mpvae_gemm="f16x3")
+y, leaves = bench.make_inputs(L, z, B, d, dev)
+for it in range(2):
+    bench.step(y, leaves, args, it)
+torch.cuda.synchronize()
+lib = H.load_library()
+buf = np.zeros((2, 8, 32, 4), np.uint64)
+fn = lib.mpv_dbg_dr_stamps
+fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
+assert fn(buf.ctypes.data) == 0
+st = buf.astype(np.int64)
+names = ["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"]
+for blk in range(2):
+    for w in range(8):
+        t = st[blk, w]
+        ph = [t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[1:, 0] - t[:-1, 3]]
+        print(f"block {blk} wave {w}: " + "  ".join(f"{n} {int(np.median(p))}" for n, p in zip(names, ph))
+              + f"  iter {int(np.median(t[1:, 0] - t[:-1, 0]))}")
