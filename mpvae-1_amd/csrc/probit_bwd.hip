@@ -283,7 +283,7 @@ __device__ unsigned long long g_dr_stamps[2][8][32][4];
   } while (0)
 #endif
 #ifndef MPV_DR_KIND
-#define MPV_DR_KIND 0  // 0: 16x16x32 ring, 1: 16x16x32 staggered, 2: 32x32x16 4-deep ring
+#define MPV_DR_KIND 1  // 0: 16x16x32 ring, 1: 16x16x32 staggered, 2: 32x32x16 4-deep ring, 3: 2 staggered
 #endif
 #ifndef MPV_DMA_ASM
 #define MPV_DMA_ASM 1
@@ -514,9 +514,7 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
                                                            (int64_t)min(q, rows - 1) * p.eps16.ld +
                                                            2 * z0);
     if (MPV_ABL & 128) continue;
-    __builtin_amdgcn_global_load_lds(src + ((lane_u ^ (r & 7)) << 5) + lane_h,
-                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
-                                     16, 0, 0);
+    lds_dma16(src, (uint32_t)(((lane_u ^ (r & 7)) << 5) + lane_h), lds_addr(dst + pc * 1024));
   }
 }
 
@@ -579,30 +577,40 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   // the two groups run the same number of barriers: 2*nst + 1
   if (grp == 0) {
     for (int i = 0; i < nst; ++i) {
+      const int ci = i;
+      MPV_STAMP(0);
       // slot 2i: stream stage i+1, read stage i
       if (i + 1 < nst)
         drs_issue<PER_WAVE, PIECES>(p, smem + ((i + 1) & 1) * STAGE, q_begin + (i + 1) * kDrKR,
                                     rows, wn, l0, z0, lane_u, lane_h);
+      MPV_STAMP(1);
       dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
       lds_barrier();
+      MPV_STAMP(2);
       // slot 2i+1: MFMAs of stage i; stage i+1 landed before the barrier
       __builtin_amdgcn_s_setprio(1);
       dr_mfma<TM, TN>(acc, f);
       __builtin_amdgcn_s_setprio(0);
       wait_vmcnt<0>();
+      MPV_STAMP(3);
       barrier_raw();
     }
     barrier_raw();
   } else {
     barrier_raw();
     for (int i = 0; i < nst; ++i) {
+      const int ci = i;
+      MPV_STAMP(0);
       // slot 2i+1: read stage i
       dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
+      MPV_STAMP(1);
       lds_barrier();
+      MPV_STAMP(2);
       // slot 2i+2: MFMAs of stage i
       __builtin_amdgcn_s_setprio(1);
       dr_mfma<TM, TN>(acc, f);
       __builtin_amdgcn_s_setprio(0);
+      MPV_STAMP(3);
       barrier_raw();
     }
   }
@@ -648,9 +656,7 @@ MPV_DEV void dr32_issue(const Dr16Params& p, char* dst, int q0, int rows, int wi
                                                            (int64_t)min(q, rows - 1) * p.eps16.ld +
                                                            2 * z0);
     if (MPV_ABL & 128) continue;
-    __builtin_amdgcn_global_load_lds(src + ((lane_u ^ dr32_swz(r)) << 5) + lane_h,
-                                     (__attribute__((address_space(3))) void*)(dst + pc * 1024),
-                                     16, 0, 0);
+    lds_dma16(src, (uint32_t)(((lane_u ^ dr32_swz(r)) << 5) + lane_h), lds_addr(dst + pc * 1024));
   }
 }
 
@@ -743,6 +749,110 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR32_kernel(Dr16Params p) {
   }
   const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
   // D[i = l][j = z], 32x32 block: reg j -> row 8*(j/4) + 4*(lane/32) + j%4, col lane%32
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int l = l0 + (wm * TM + m) * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+        const int zc = z0 + (wn * TN + n) * 32 + (lane & 31);
+        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][j] * inv;
+      }
+}
+
+// Staggered 32x32x16 dR: 16-row stages in a 4-deep ring, the two wave groups
+// (wm = 0, 1; paired on the SIMDs) one slot apart.  Group g does mem(j) in slot
+// 2j+g and mma(j) in slot 2j+g+1; each slot ends with one barrier.
+//   mem(j): LDS-DMA of this wave's share of stage j+3 into image (j+3)%4 (it held
+//           stage j-1, read in slots 2j-2 / 2j-1), fragment reads of stage j.
+//   mma(j): 24 MFMAs; then wait until this wave's pieces of stage j+2 landed,
+//           so stage j+2 is complete after the barrier that precedes its first
+//           read (slot 2j+4).
+// DMA is spread over every wave and every slot, with ~2 slot pairs of slack.
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(WM* WN * 64, 1) void dR32s_kernel(Dr16Params p) {
+  static_assert(WM == 2, "two wave groups");
+  constexpr int NW = WM * WN;
+  constexpr int BL = WM * TM * 32, BZ = WN * TN * 32;
+  static_assert(BL == 256 && BZ == 256, "256 x 256 tile");
+  constexpr int ROWB = BL * 4;
+  constexpr int IMG = kDr32KR * ROWB;   // 16 KB per operand
+  constexpr int STAGE = 2 * IMG;        // 32 KB
+  constexpr int PIECES = STAGE / 1024;  // 32 rows of 1 KB
+  static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
+  constexpr int PER_WAVE = PIECES / NW;
+  __shared__ __attribute__((aligned(1024))) char smem[kDr32NS * STAGE];
+
+  int kc, tile;
+  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
+  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int grp = wm;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tq = lr >> 2, tp = lr & 3;
+  const int rows = p.B * p.S;
+  const int q_begin = kc * p.rows_per_chunk;
+  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
+  const int lane_u = lane >> 1, lane_h = (lane & 1) * 16;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[m][n][j] = 0.0f;
+
+  const int nst = (q_end - q_begin + kDr32KR - 1) / kDr32KR;
+  for (int j = 0; j < 3 && j < nst; ++j)
+    dr32_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDr32KR, rows, wid, l0, z0,
+                                 lane_u, lane_h);
+  // stages 0 and 1 complete (own pieces; stage 2 may fly), then everyone: the
+  // loop's own waits start with stage 2 (end of mma(0))
+  wait_vmcnt_dyn(max(0, min(3, nst) - 2) * PER_WAVE);
+  barrier_raw();
+  if (grp == 1) barrier_raw();  // group 1 runs one slot behind
+  Dr32Frag<TM, TN> f;
+  for (int j = 0; j < nst; ++j) {
+    // ---- mem(j)
+    if (j + 3 < nst)
+      dr32_issue<PER_WAVE, PIECES>(p, smem + ((j + 3) & 3) * STAGE, q_begin + (j + 3) * kDr32KR,
+                                   rows, wid, l0, z0, lane_u, lane_h);
+    const char* base = smem + (j & 3) * STAGE;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      f.ah[m] = dr32_frag<ROWB>(base, wm * TM + m, 0, lg, tq, tp);
+      f.al[m] = dr32_frag<ROWB>(base, wm * TM + m, 2, lg, tq, tp);
+    }
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      f.bh[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 0, lg, tq, tp);
+      f.bl[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 2, lg, tq, tp);
+    }
+    lds_barrier();
+    // ---- mma(j)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                           acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    // own pieces of stage j+2 landed; stages j+3 (issued this round) may fly
+    if (j + 2 < nst) wait_vmcnt_dyn(min(1, nst - 1 - (j + 2)) * PER_WAVE);
+    barrier_raw();
+  }
+  if (grp == 0) barrier_raw();  // same barrier count for both groups
+  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -1090,7 +1200,9 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.rows_pad = pl.rows_pad;
       // 256 x 256 tile, 8 waves of 128 x 64, 2-stage ring (128 KB LDS)
       static_assert(kDr16Tile == 256, "launch config below");
-      if (MPV_DR_KIND == 2)
+      if (MPV_DR_KIND == 3)
+        MPV_LAUNCH("dR_gemm", (dR32s_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
+      else if (MPV_DR_KIND == 2)
         MPV_LAUNCH("dR_gemm", (dR32_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
       else if (MPV_DR_KIND == 1)
         MPV_LAUNCH("dR_gemm", (dR16s_kernel<2, 4, 8, 4>), dim3((unsigned)blocks), dim3(512), 0, st, dp);

@@ -33,7 +33,9 @@ fn = lib.mpv_dbg_dr_stamps
 fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
 assert fn(buf.ctypes.data) == 0
 st = buf.astype(np.int64)
-names = ["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"]
+KIND = int(os.environ.get("STAMP_KIND", "0"))
+names = (["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"] if KIND == 0 else
+         ["A:issue|B:reads", "A:reads+bar|B:bar", "A:mfma+wait|B:mfma", "bar->next"])
 for blk in range(2):
     for w in range(8):
         t = st[blk, w]
