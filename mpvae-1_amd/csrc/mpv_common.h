@@ -108,6 +108,46 @@ MPV_DEV f32x2 probit_eval2(f32x2 u, f32x2& phi) {
   return cdf * kC1 + splat2(kC0);
 }
 
+// probit_eval2 on N independent pairs in lockstep (step-major): dependent
+// packed ops need a wait state between them, and N interleaved chains hide it.
+// Bit-identical to N probit_eval2 calls.
+template <int N>
+MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N]) {
+#pragma clang fp contract(off)
+  f32x2 z[N], t[N], p[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) z[j] = f32x2{fabsf(u[j].x), fabsf(u[j].y)} * kInvSqrt2;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 den = pk_fma(splat2(0.5f), z[j], splat2(1.0f));
+    t[j] = f32x2{fast_rcp(den.x), fast_rcp(den.y)};
+  }
+  constexpr float c[10] = {0.17087277f, -0.82215223f, 1.48851587f, -1.13520398f, 0.27886807f,
+                           -0.18628806f, 0.09678418f, 0.37409196f, 1.00002368f, -1.26551223f};
+#pragma unroll
+  for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
+#pragma unroll
+  for (int k = 2; k < 10; ++k)
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], p[j], splat2(c[k]));
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 az = (-z[j] * z[j]) * 1.4426950408889634f;
+    const f32x2 ap = p[j] * 1.4426950408889634f;
+    const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
+    const f32x2 ep = f32x2{__builtin_amdgcn_exp2f(ap.x), __builtin_amdgcn_exp2f(ap.y)};
+    phi[j] = ez * kInvSqrt2Pi;
+    z[j] = (t[j] * ez) * ep;  // erfc
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 om = splat2(1.0f) - z[j];
+    const f32x2 erf_u = f32x2{u[j].x < 0.0f ? -om.x : om.x, u[j].y < 0.0f ? -om.y : om.y};
+    const f32x2 cdf = splat2(0.5f) * (splat2(1.0f) + erf_u);
+    E[j] = cdf * kC1 + splat2(kC0);
+  }
+}
+
 // ---- DPP row (16-lane) reductions ------------------------------------------
 // row_shr:n = 0x110 + n.  After the 4 steps lane 15 of every 16-lane row holds
 // the row's sum (bound_ctrl: lanes shifted in from outside the row read 0).
@@ -121,6 +161,17 @@ MPV_DEV float row16_sum_to_lane15(float v) {
   v += dpp_f<0x114>(v);   // row_shr:4
   v += dpp_f<0x118>(v);   // row_shr:8
   return v;
+}
+
+// Sum over the four 16-lane rows of the wave (lanes l, l^16, l^32, l^48) by
+// the gfx950 row-swap permutes (VALU, no LDS): every lane gets the total.
+MPV_DEV float sum_lanegroups(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
 }
 
 MPV_DEV float wave_sum(float v) {

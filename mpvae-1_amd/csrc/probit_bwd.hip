@@ -106,24 +106,32 @@ struct ElemParams {
 // (packed fp32): u = t + base, E = probit(u),
 //   dE = alpha (y/E - (1-y)/(1-E)) + [y=1](-betaP) e^{-5E} + [y=0] betaN e^{5E} + g_ind
 // (mpvae.py:110-117, 184-185 differentiated), dL/dt = dE (1-1e-6) phi(u).
-MPV_DEV f32x2 d_elem2(float t, f32x2 base, float y, bool soft, f32x2 alpha, f32x2 bP, f32x2 bN,
-                      f32x2 gind) {
-  f32x2 phi;
-  const f32x2 E = probit_eval2(splat2(t) + base, phi);
-  // d logp / dE = y/E - (1-y)/(1-E): one reciprocal for a 0/1 label
-  const f32x2 q = (y == 0.0f) ? splat2(1.0f) - E : E;
-  f32x2 dl = f32x2{fast_rcp(q.x), fast_rcp(q.y)};
-  if (y == 0.0f) dl = -dl;
-  if (soft) dl = splat2(y) / E - splat2(1.0f - y) / (splat2(1.0f) - E);
-  f32x2 dE = pk_fma(alpha, dl, gind);
-  // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-  const f32x2 rk = (y == 1.0f) ? -bP : ((y == 0.0f) ? bN : splat2(0.0f));
-  const f32x2 a = E * (y == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
-  dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
-  // a degenerate row poisons every label, whatever its value (reference autograd)
-  if (bP.x != bP.x) dE.x = bP.x;
-  if (bP.y != bP.y) dE.y = bP.y;
-  return (dE * kC1) * phi;
+// Four elements (columns) of one row at once, step-major so that the
+// dependent packed ops of one element interleave with the others'.
+MPV_DEV void d_elem2x4(const float (&t)[4], const f32x2 (&base)[4], const float (&y)[4],
+                       const bool (&soft)[4], f32x2 alpha, f32x2 bP, f32x2 bN,
+                       const f32x2 (&gind)[4], f32x2 (&out)[4]) {
+  f32x2 u[4], E[4], phi[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + base[q];
+  probit_eval2xN<4>(u, E, phi);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    // d logp / dE = y/E - (1-y)/(1-E): one reciprocal for a 0/1 label
+    const f32x2 d = (y[q] == 0.0f) ? splat2(1.0f) - E[q] : E[q];
+    f32x2 dl = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
+    if (y[q] == 0.0f) dl = -dl;
+    if (soft[q]) dl = splat2(y[q]) / E[q] - splat2(1.0f - y[q]) / (splat2(1.0f) - E[q]);
+    f32x2 dE = pk_fma(alpha, dl, gind[q]);
+    // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
+    const f32x2 rk = (y[q] == 1.0f) ? -bP : ((y[q] == 0.0f) ? bN : splat2(0.0f));
+    const f32x2 a = E[q] * (y[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+    dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
+    // a degenerate row poisons every label, whatever its value (reference autograd)
+    if (bP.x != bP.x) dE.x = bP.x;
+    if (bP.y != bP.y) dE.y = bP.y;
+    out[q] = (dE * kC1) * phi[q];
+  }
 }
 
 // Inputs of one row s of the element pass: its six coefficients (label .x,
@@ -177,6 +185,12 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     soft[q] = !(yv[q] == 0.0f || yv[q] == 1.0f);
   }
   float se[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x2 base2[4], gind2[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    base2[q] = f32x2{fe[q], fx[q]};
+    gind2[q] = f32x2{gil[q], gi[q]};
+  }
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
   if (active && c0 < p.Lc) {
@@ -188,13 +202,13 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
       if (s + p.RPI < s_end) elem_row_load<VEC>(nxt, p, b, s + p.RPI, c0, ok);
       const int64_t cb = (int64_t)b * S + s;
       float G[4];
+      f32x2 g2[4];
+      d_elem2x4(cur.t, base2, yv, soft, cur.alpha, cur.bP, cur.bN, gind2, g2);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x2 g2 = d_elem2(cur.t[q], f32x2{fe[q], fx[q]}, yv[q], soft[q], cur.alpha,
-                                 cur.bP, cur.bN, f32x2{gil[q], gi[q]});
-        se[q] += ok[q] ? g2.x : 0.0f;
-        sx[q] += ok[q] ? g2.y : 0.0f;
-        G[q] = ok[q] ? g2.x + g2.y : 0.0f;
+        se[q] += ok[q] ? g2[q].x : 0.0f;
+        sx[q] += ok[q] ? g2[q].y : 0.0f;
+        G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
       }
       if (PLANES) {
         uint16_t h[4], l[4];

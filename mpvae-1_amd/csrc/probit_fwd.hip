@@ -47,6 +47,33 @@ struct FwdParams {
 #ifndef MPV_ABL
 #define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
 #endif
+#ifndef MPV_FWD_T
+#define MPV_FWD_T 1
+#endif
+
+// In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
+// points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
+#if (MPV_ABL & 1024)
+__device__ unsigned long long g_fwd_stamps[2][4][32][4];
+__device__ unsigned long long g_fwd_epi[2][4][8][2];
+#define FWD_STAMP(k)                                                                  \
+  do {                                                                                \
+    if (blockIdx.x < 2 && gs >= 256 && gs < 288 && (threadIdx.x & 63) == 0)           \
+      g_fwd_stamps[blockIdx.x][threadIdx.x >> 6][gs - 256][k] = __builtin_readcyclecounter(); \
+  } while (0)
+#define FWD_ESTAMP(k)                                                                 \
+  do {                                                                                \
+    if (blockIdx.x < 2 && st - t_begin >= 8 && st - t_begin < 16 && (threadIdx.x & 63) == 0) \
+      g_fwd_epi[blockIdx.x][threadIdx.x >> 6][st - t_begin - 8][k] = __builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define FWD_STAMP(k) \
+  do {               \
+  } while (0)
+#define FWD_ESTAMP(k) \
+  do {                \
+  } while (0)
+#endif
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
@@ -585,6 +612,7 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
       for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int kc = 0; kc < nK; ++kc, ++gs) {
+      FWD_STAMP(0);
       // stage gs must have landed; later stages may stay in flight (loads
       // retire in order, so stores issued after them need not be waited for)
       if (NSTAGE == 2)
@@ -592,12 +620,16 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
       else
         wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * my_pieces);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      FWD_STAMP(1);
       barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      FWD_STAMP(2);
       dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+      FWD_STAMP(3);
       Frag16<TM, TN> f;
       fwd16_read<TM, TN, BM>(f, smem + (gs % NSTAGE) * STAGE, wm, wn, lr, coh, col);
       fwd16_mfma<TM, TN>(acc, f);
     }
+    FWD_ESTAMP(0);
     if (MPV_ABL & 1) {
       float v = 0.f;
 #pragma unroll
@@ -608,8 +640,279 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
     } else {
       fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, st * BM, nt, red, cols);
     }
+    FWD_ESTAMP(1);
   }
   fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, red);
+}
+
+// ------------------------------------------ 3xf16, transposed accumulators
+// The same GEMM with the roles of the operands swapped: MFMA-M = labels (R
+// rows), MFMA-N = samples (eps rows).  A lane then holds 4 consecutive labels
+// of one sample, which makes the epilogue cheap where it was costly:
+//   * the 6 row statistics of a sample sum over labels in-lane, then over the
+//     4 lane rows with two row-swap permutes (was: 16-lane DPP trees per row);
+//   * T is stored as one 16-B vector per (sample, 4 labels);
+//   * column sums over samples reduce once per label group into LDS.
+template <int TL, int TS>
+struct FragT {
+  s16x8 rh[TL], rl[TL], eh[TS], el[TS];  // R (labels) and eps (samples), hi / lo
+};
+
+template <int WL, int TL, int TS, int BM>
+MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int ws, int lr, int coh,
+                         int col) {
+#pragma unroll
+  for (int m = 0; m < TL; ++m) {
+    const int off = (BM + (wl * TL + m) * 16 + lr) * kRowB;
+    f.rh[m] = *reinterpret_cast<const s16x8*>(base + off + coh);
+    f.rl[m] = *reinterpret_cast<const s16x8*>(base + off + col);
+  }
+#pragma unroll
+  for (int n = 0; n < TS; ++n) {
+    const int off = ((ws * TS + n) * 16 + lr) * kRowB;
+    f.eh[n] = *reinterpret_cast<const s16x8*>(base + off + coh);
+    f.el[n] = *reinterpret_cast<const s16x8*>(base + off + col);
+  }
+}
+
+template <int TL, int TS>
+MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < TS; ++n) {
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
+                                                         acc[m][n], 0, 0, 0);
+    }
+}
+
+// acc[m][n][i] = t of sample (ws*TS+n)*16 + lr, label (wl*TL+m)*16 + 4*lg + i.
+// Masks are carried as 0/1 float weights (VGPRs) rather than lane masks: the
+// 16 per-label masks of a label group would otherwise pin ~40 SGPRs and spill.
+// Every element is finite (R pad rows are zero, eps rows are clamped), so
+// weighting instead of selecting is exact.
+template <int WL, int WS, int TL, int TS>
+MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
+                                 int b, int s0, int s_own, int nt, float* red, float* cacc,
+                                 const float* cols, bool soft_any) {
+  constexpr int NT = WL * WS * 64, BM = WS * TS * 16, BN = WL * TL * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wl = wid % WL, ws = wid / WL, lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, B = p.B, L = p.L, n0 = nt * BN;
+  f32x2 sl[TS], sp[TS], sn[TS];  // per sample: log-prob, P, N (label .x / feature .y branch)
+#pragma unroll
+  for (int n = 0; n < TS; ++n) sl[n] = sp[n] = sn[n] = splat2(0.0f);
+  const bool vecT = p.T != nullptr && (L & 3) == 0;
+  // one label group per iteration, not unrolled (code size / live ranges):
+  // the group's accumulators are always acc[0]; the rest rotate down after it
+#pragma unroll 1
+  for (int m = 0; m < TL; ++m) {
+    f32x4 am[TS];
+#pragma unroll
+    for (int n = 0; n < TS; ++n) am[n] = acc[0][n];
+#pragma unroll
+    for (int mm = 0; mm + 1 < TL; ++mm)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + 1][n];
+    const int lb = (wl * TL + m) * 16 + lg * 4;  // first of the lane's 4 labels in the tile
+    const f32x4 fe4 = *reinterpret_cast<const f32x4*>(cols + lb);
+    const f32x4 fx4 = *reinterpret_cast<const f32x4*>(cols + BN + lb);
+    const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
+    float wok[4], wpos[4], wneg[4], sg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wok[i] = n0 + lb + i < L ? 1.0f : 0.0f;
+      wpos[i] = y4[i] == 1.0f ? wok[i] : 0.0f;
+      wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
+      sg[i] = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
+    }
+    const int last_ok = n0 + lb + 3 < L;
+    f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
+#pragma unroll
+    for (int n = 0; n < TS; ++n) {
+      const int s = s0 + (ws * TS + n) * 16 + lr;
+      const bool rowok = s >= s_own && s < S;
+      const float wr = rowok ? 1.0f : 0.0f;
+      const f32x4 t4 = am[n] * scale;
+      if (!(MPV_ABL & 2) && p.T != nullptr && rowok) {
+        float* dst = p.T + ((int64_t)b * S + s) * L + n0 + lb;
+        if (vecT && last_ok) {
+          *reinterpret_cast<f32x4*>(dst) = t4;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n0 + lb + i < L) dst[i] = t4[i];
+        }
+      }
+      f32x2 uu[4], E4[4], phi4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + f32x2{fe4[i], fx4[i]};
+      probit_eval2xN<4>(uu, E4, phi4);
+      f32x2 lp[4], r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x2 E = E4[i];
+        const float y = y4[i];
+        // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
+        const f32x2 q = (y == 0.0f) ? splat2(1.0f) - E : E;
+        lp[i] = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)} *
+                0.6931471805599453f;
+        // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
+        const f32x2 a = E * sg[i];
+        r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+      }
+      if (soft_any) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float y = y4[i];
+          if (!(y == 0.0f || y == 1.0f)) {
+            const f32x2 E = E4[i];
+            lp[i].x = y * fast_log(E.x) + (1.0f - y) * fast_log(1.0f - E.x);
+            lp[i].y = y * fast_log(E.y) + (1.0f - y) * fast_log(1.0f - E.y);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sl[n] = pk_fma(splat2(wr * wok[i]), lp[i], sl[n]);
+        sp[n] = pk_fma(splat2(wr * wpos[i]), r[i], sp[n]);
+        sn[n] = pk_fma(splat2(wr * wneg[i]), r[i], sn[n]);
+        ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one sample at a time: bounded live ranges
+    }
+    // column sums of these 4 labels over the wave's samples: 16-lane trees,
+    // lane 15 of each row accumulates into the (ws, label) slot it owns
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
+      if (lr == 15) {
+        float* c = cacc + (ws * BN + lb + i) * 2;
+        c[0] += e;
+        c[1] += x;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
+  }
+  // row statistics: sum over the 4 lane rows; lanes of row 0 publish
+#pragma unroll
+  for (int n = 0; n < TS; ++n) {
+    const float v[6] = {sl[n].x, sl[n].y, sp[n].x, sn[n].x, sp[n].y, sn[n].y};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float tot = sum_lanegroups(v[k]);
+      if (lg == 0) red[(wl * BM + (ws * TS + n) * 16 + lr) * 6 + k] = tot;
+    }
+  }
+  lds_barrier();
+  for (int r = tid; r < BM; r += NT) {
+    const int s = s0 + r;
+    if (s >= s_own && s < S) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < WL; ++w) v += red[(w * BM + r) * 6 + k];
+        p.rowpart[(((int64_t)k * p.nNt + nt) * B + b) * S + s] = v;
+      }
+    }
+  }
+  lds_barrier();
+}
+
+template <int WL, int WS, int TL, int TS, int NSTAGE>
+__global__ __launch_bounds__(WL* WS * 64, 2) void probit_fwd16t_kernel(FwdParams p) {
+  constexpr int NW = WL * WS;
+  constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
+  constexpr int STAGE = (BM + BN) * kRowB;
+  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN) * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL, ws = wid / WL;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  // does the label tile hold soft (non 0/1) labels?  (uniform; enables the
+  // two-log BCE path of the epilogue)
+  bool my_soft = false;
+  for (int i = tid; i < BN; i += NW * 64) {
+    const int l = n0 + i;
+    if (l < p.L) {
+      const float yv = p.y[(int64_t)b * p.L + l];
+      my_soft |= !(yv == 0.0f || yv == 1.0f);
+    }
+  }
+  const bool soft_any = __syncthreads_or(my_soft);
+  Fwd16Dma<BM, BN, NW> dma;
+  dma.init(p, t_begin, b, n0, wid, lane);
+#pragma unroll
+  for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+
+  int gs = 0;
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TS];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
+      FWD_STAMP(0);
+      if (NSTAGE == 2)
+        wait_vmcnt<0>();
+      else
+        wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * dma.per_wave());
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      FWD_STAMP(1);
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      FWD_STAMP(2);
+      dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+      FWD_STAMP(3);
+      FragT<TL, TS> f;
+      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
+      fwd16t_mfma<TL, TS>(acc, f);
+    }
+    FWD_ESTAMP(0);
+    fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                        soft_any);
+    FWD_ESTAMP(1);
+  }
+  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
+  lds_barrier();
+  for (int c = tid; c < BN; c += NW * 64) {
+    const int l = n0 + c;
+    if (l < p.L) {
+      float e = 0.f, x = 0.f;
+#pragma unroll
+      for (int w = 0; w < WS; ++w) {
+        e += cacc[(w * BN + c) * 2 + 0];
+        x += cacc[(w * BN + c) * 2 + 1];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + l] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + l] = x;
+    }
+  }
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
@@ -763,7 +1066,12 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 1:  // BN 96, 8 waves, 4-stage ring (112 KB)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
         break;
-      default:  // 128 x 128 tile, 4 waves of 64 x 64 (3 MFMAs per 1.33 fragment
+      default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
+        if (MPV_FWD_T) {
+          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
+          break;
+        }
+        // 128 x 128 tile, 4 waves of 64 x 64 (3 MFMAs per 1.33 fragment
                 // reads), 2-stage ring (64 KB): 2 workgroups per CU, so one
                 // workgroup's epilogue (VALU) overlaps the other's MFMA phase
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
@@ -788,6 +1096,15 @@ static int check_split_operand(const mpv_split16& o, int64_t rows, int64_t ld_mi
 using namespace mpv;
 
 extern "C" {
+
+#if (MPV_ABL & 1024)
+int mpv_dbg_fwd_stamps(void* host_out, void* host_epi) {
+  return (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) ==
+                  hipSuccess &&
+          hipMemcpyFromSymbol(host_epi, HIP_SYMBOL(g_fwd_epi), sizeof(g_fwd_epi)) == hipSuccess)
+             ? 0 : 1;
+}
+#endif
 
 size_t mpv_fwd_workspace_bytes(const mpv_shape* shape) {
   if (check_shape(shape) != MPV_OK) return 0;
