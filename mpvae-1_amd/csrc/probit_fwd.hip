@@ -706,7 +706,31 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   f32x2 sl[TS], sp[TS], sn[TS];  // per sample: log-prob, P, N (label .x / feature .y branch)
 #pragma unroll
   for (int n = 0; n < TS; ++n) sl[n] = sp[n] = sn[n] = splat2(0.0f);
-  const bool vecT = p.T != nullptr && (L & 3) == 0;
+  // T stash first, all label groups of a sample back to back: the 4 lane rows
+  // x TL groups cover whole 128-B lines of the sample's T row (written while
+  // still combinable in L2, rather than as half lines far apart in time)
+  if (!(MPV_ABL & 2) && p.T != nullptr) {
+    const bool vecT = (L & 3) == 0;
+#pragma unroll
+    for (int n = 0; n < TS; ++n) {
+      const int s = s0 + (ws * TS + n) * 16 + lr;
+      if (s >= s_own && s < S) {
+        float* row = p.T + ((int64_t)b * S + s) * L + n0;
+#pragma unroll
+        for (int m = 0; m < TL; ++m) {
+          const int lb = (wl * TL + m) * 16 + lg * 4;
+          const f32x4 t4 = acc[m][n] * scale;
+          if (vecT && n0 + lb + 3 < L) {
+            *reinterpret_cast<f32x4*>(row + lb) = t4;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (n0 + lb + i < L) row[lb + i] = t4[i];
+          }
+        }
+      }
+    }
+  }
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
 #pragma unroll 1
@@ -730,7 +754,6 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
       sg[i] = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
     }
-    const int last_ok = n0 + lb + 3 < L;
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
@@ -738,20 +761,15 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       const bool rowok = s >= s_own && s < S;
       const float wr = rowok ? 1.0f : 0.0f;
       const f32x4 t4 = am[n] * scale;
-      if (!(MPV_ABL & 2) && p.T != nullptr && rowok) {
-        float* dst = p.T + ((int64_t)b * S + s) * L + n0 + lb;
-        if (vecT && last_ok) {
-          *reinterpret_cast<f32x4*>(dst) = t4;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n0 + lb + i < L) dst[i] = t4[i];
-        }
-      }
       f32x2 uu[4], E4[4], phi4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + f32x2{fe4[i], fx4[i]};
-      probit_eval2xN<4>(uu, E4, phi4);
+      if (MPV_ABL & 4096) {  // timing study: no probit
+#pragma unroll
+        for (int i = 0; i < 4; ++i) E4[i] = uu[i] * 0.01f + splat2(0.5f);
+      } else {
+        probit_eval2xN<4>(uu, E4, phi4);
+      }
       f32x2 lp[4], r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -789,6 +807,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     // lane 15 of each row accumulates into the (ws, label) slot it owns
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if (MPV_ABL & 8192) {
+        if (lr == 15) cacc[(ws * BN + lb + i) * 2] += ce[i].x + ce[i].y;
+        continue;
+      }
       const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
       if (lr == 15) {
         float* c = cacc + (ws * BN + lb + i) * 2;
