@@ -148,6 +148,34 @@ MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N])
   }
 }
 
+// Scalar lockstep version (N independent evaluations, no packed ops):
+// bit-identical to N probit_eval calls (phi omitted).
+template <int N>
+MPV_DEV void probit_probN(const float (&u)[N], float (&E)[N]) {
+  float z[N], t[N], p[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    z[j] = fabsf(u[j]) * kInvSqrt2;
+    t[j] = fast_rcp(fmaf(0.5f, z[j], 1.0f));
+  }
+  constexpr float c[10] = {0.17087277f, -0.82215223f, 1.48851587f, -1.13520398f, 0.27886807f,
+                           -0.18628806f, 0.09678418f, 0.37409196f, 1.00002368f, -1.26551223f};
+#pragma unroll
+  for (int j = 0; j < N; ++j) p[j] = fmaf(t[j], c[0], c[1]);
+#pragma unroll
+  for (int k = 2; k < 10; ++k)
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = fmaf(t[j], p[j], c[k]);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float ez = fast_exp(-z[j] * z[j]);
+    const float erfc_z = t[j] * ez * fast_exp(p[j]);
+    const float erf_u = u[j] < 0.0f ? __fsub_rn(erfc_z, 1.0f) : __fsub_rn(1.0f, erfc_z);
+    const float cdf = __fmul_rn(0.5f, __fadd_rn(1.0f, erf_u));
+    E[j] = __fadd_rn(__fmul_rn(cdf, kC1), kC0);
+  }
+}
+
 // ---- DPP row (16-lane) reductions ------------------------------------------
 // row_shr:n = 0x110 + n.  After the 4 steps lane 15 of every 16-lane row holds
 // the row's sum (bound_ctrl: lanes shifted in from outside the row read 0).

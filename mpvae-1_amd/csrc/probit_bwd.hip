@@ -20,6 +20,10 @@
 #include "abi_util.h"
 #include "mpv_common.h"
 
+#ifndef MPV_ABL
+#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
+#endif
+
 namespace mpv {
 
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
@@ -106,31 +110,51 @@ struct ElemParams {
 // (packed fp32): u = t + base, E = probit(u),
 //   dE = alpha (y/E - (1-y)/(1-E)) + [y=1](-betaP) e^{-5E} + [y=0] betaN e^{5E} + g_ind
 // (mpvae.py:110-117, 184-185 differentiated), dL/dt = dE (1-1e-6) phi(u).
+// Per-column constants of the element pass (the lane's four label columns).
+struct ElemCol {
+  f32x2 base[4];  // fe_out, fx_out
+  f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total
+  float y[4];
+  bool soft[4];
+  float sdl[4];   // sign of d logp/dE for a 0/1 label: -1 for y = 0, +1 otherwise
+  float sgx[4];   // e^{-5E} (y = 1) or e^{5E}: exponent multiplier in log2 units
+  float wp[4], wn[4];  // [y = 1], [y = 0]
+};
+
 // Four elements (columns) of one row at once, step-major so that the
 // dependent packed ops of one element interleave with the others'.
-MPV_DEV void d_elem2x4(const float (&t)[4], const f32x2 (&base)[4], const float (&y)[4],
-                       const bool (&soft)[4], f32x2 alpha, f32x2 bP, f32x2 bN,
-                       const f32x2 (&gind)[4], f32x2 (&out)[4]) {
+MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
+                       f32x2 (&out)[4]) {
   f32x2 u[4], E[4], phi[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + base[q];
+  for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + c.base[q];
   probit_eval2xN<4>(u, E, phi);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // d logp / dE = y/E - (1-y)/(1-E): one reciprocal for a 0/1 label
-    const f32x2 d = (y[q] == 0.0f) ? splat2(1.0f) - E[q] : E[q];
-    f32x2 dl = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
-    if (y[q] == 0.0f) dl = -dl;
-    if (soft[q]) dl = splat2(y[q]) / E[q] - splat2(1.0f - y[q]) / (splat2(1.0f) - E[q]);
-    f32x2 dE = pk_fma(alpha, dl, gind[q]);
+    const f32x2 d = (c.y[q] == 0.0f) ? splat2(1.0f) - E[q] : E[q];
+    const f32x2 r = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
+    f32x2 dE;
+    if (c.soft[q]) {
+      const f32x2 dl =
+          splat2(c.y[q]) / E[q] - splat2(1.0f - c.y[q]) / (splat2(1.0f) - E[q]);
+      dE = pk_fma(alpha, dl, c.gind[q]);
+    } else {
+      dE = pk_fma(alpha * c.sdl[q], r, c.gind[q]);
+    }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-    const f32x2 rk = (y[q] == 1.0f) ? -bP : ((y[q] == 0.0f) ? bN : splat2(0.0f));
-    const f32x2 a = E[q] * (y[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+    const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(-c.wp[q]) * bP);
+    const f32x2 a = E[q] * c.sgx[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
-    // a degenerate row poisons every label, whatever its value (reference autograd)
-    if (bP.x != bP.x) dE.x = bP.x;
-    if (bP.y != bP.y) dE.y = bP.y;
     out[q] = (dE * kC1) * phi[q];
+  }
+  // a degenerate row poisons every label, whatever its value (reference autograd)
+  if (bP.x != bP.x || bP.y != bP.y) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (bP.x != bP.x) out[q].x = bP.x;
+      if (bP.y != bP.y) out[q].y = bP.y;
+    }
   }
 }
 
@@ -185,32 +209,45 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     soft[q] = !(yv[q] == 0.0f || yv[q] == 1.0f);
   }
   float se[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
-  f32x2 base2[4], gind2[4];
+  ElemCol ec;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    base2[q] = f32x2{fe[q], fx[q]};
-    gind2[q] = f32x2{gil[q], gi[q]};
+    ec.base[q] = f32x2{fe[q], fx[q]};
+    ec.gind[q] = f32x2{gil[q], gi[q]};
+    ec.y[q] = yv[q];
+    ec.soft[q] = soft[q];
+    ec.sdl[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
+    ec.sgx[q] = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+    ec.wp[q] = yv[q] == 1.0f ? 1.0f : 0.0f;
+    ec.wn[q] = yv[q] == 0.0f ? 1.0f : 0.0f;
   }
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
   if (active && c0 < p.Lc) {
-    // one row of lookahead: row s+RPI's loads are in flight while row s computes
-    const int s0 = s_begin + rsub;
-    ElemRow cur, nxt;
+    // two rows of lookahead: rows s+RPI and s+2RPI are in flight while row s
+    // computes (the element math and the T stream overlap)
+    const int s0 = s_begin + rsub, R = p.RPI;
+    ElemRow cur, nx1, nx2;
     if (s0 < s_end) elem_row_load<VEC>(cur, p, b, s0, c0, ok);
-    for (int s = s0; s < s_end; s += p.RPI) {
-      if (s + p.RPI < s_end) elem_row_load<VEC>(nxt, p, b, s + p.RPI, c0, ok);
+    if (s0 + R < s_end) elem_row_load<VEC>(nx1, p, b, s0 + R, c0, ok);
+    for (int s = s0; s < s_end; s += R) {
+      if (s + 2 * R < s_end) elem_row_load<VEC>(nx2, p, b, s + 2 * R, c0, ok);
       const int64_t cb = (int64_t)b * S + s;
       float G[4];
       f32x2 g2[4];
-      d_elem2x4(cur.t, base2, yv, soft, cur.alpha, cur.bP, cur.bN, gind2, g2);
+      if (MPV_ABL & 16384) {  // timing study: no element math
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g2[q] = splat2(cur.t[q]) * cur.alpha + ec.base[q];
+      } else {
+        d_elem2x4(cur.t, ec, cur.alpha, cur.bP, cur.bN, g2);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         se[q] += ok[q] ? g2[q].x : 0.0f;
         sx[q] += ok[q] ? g2[q].y : 0.0f;
         G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
       }
-      if (PLANES) {
+      if (PLANES && !(MPV_ABL & 32768)) {
         uint16_t h[4], l[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
@@ -229,7 +266,8 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
             if (ok[q]) row[c0 + q] = G[q];
         }
       }
-      cur = nxt;
+      cur = nx1;
+      nx1 = nx2;
     }
   }
   // column sums over this block's rows: reduce the RPI row-lanes per column
@@ -279,9 +317,6 @@ struct Dr16Params {
   int nLt, nZt, nKc, rows_per_chunk, rows_pad;
 };
 
-#ifndef MPV_ABL
-#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
-#endif
 // In-kernel phase stamps (timing studies only, MPV_ABL & 1024): s_memtime at
 // the loop's phase points of blocks 0-1, iterations 256..287, every wave.
 #if (MPV_ABL & 1024)

@@ -50,6 +50,9 @@ struct FwdParams {
 #ifndef MPV_FWD_T
 #define MPV_FWD_T 1
 #endif
+#ifndef MPV_FWD_SCALAR
+#define MPV_FWD_SCALAR 0
+#endif
 
 // In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
 // points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
@@ -761,6 +764,43 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       const bool rowok = s >= s_own && s < S;
       const float wr = rowok ? 1.0f : 0.0f;
       const f32x4 t4 = am[n] * scale;
+#if MPV_FWD_SCALAR
+      // scalar path: 8 probits (4 labels x 2 branches) in lockstep
+      float u8[8], E8[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u8[2 * i] = t4[i] + fe4[i];
+        u8[2 * i + 1] = t4[i] + fx4[i];
+      }
+      probit_probN<8>(u8, E8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float y = y4[i];
+        float le, lx;
+        if (y == 0.0f) {
+          le = fast_log(1.0f - E8[2 * i]);
+          lx = fast_log(1.0f - E8[2 * i + 1]);
+        } else {
+          le = fast_log(E8[2 * i]);
+          lx = fast_log(E8[2 * i + 1]);
+        }
+        if (soft_any && !(y == 0.0f || y == 1.0f)) {
+          le = y * fast_log(E8[2 * i]) + (1.0f - y) * fast_log(1.0f - E8[2 * i]);
+          lx = y * fast_log(E8[2 * i + 1]) + (1.0f - y) * fast_log(1.0f - E8[2 * i + 1]);
+        }
+        const float re = __builtin_amdgcn_exp2f(E8[2 * i] * sg[i]);
+        const float rx = __builtin_amdgcn_exp2f(E8[2 * i + 1] * sg[i]);
+        const float wo = wr * wok[i], wp = wr * wpos[i], wq = wr * wneg[i];
+        sl[n].x = fmaf(wo, le, sl[n].x);
+        sl[n].y = fmaf(wo, lx, sl[n].y);
+        sp[n].x = fmaf(wp, re, sp[n].x);
+        sp[n].y = fmaf(wp, rx, sp[n].y);
+        sn[n].x = fmaf(wq, re, sn[n].x);
+        sn[n].y = fmaf(wq, rx, sn[n].y);
+        ce[i].x = fmaf(wr, E8[2 * i], ce[i].x);
+        ce[i].y = fmaf(wr, E8[2 * i + 1], ce[i].y);
+      }
+#else
       f32x2 uu[4], E4[4], phi4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + f32x2{fe4[i], fx4[i]};
@@ -801,6 +841,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         sn[n] = pk_fma(splat2(wr * wneg[i]), r[i], sn[n]);
         ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
       }
+#endif
       __builtin_amdgcn_sched_barrier(0);  // one sample at a time: bounded live ranges
     }
     // column sums of these 4 labels over the wave's samples: 16-lane trees,

@@ -1,18 +1,21 @@
 #!/bin/bash
 # Timing ablations of the GEMM kernels: builds libmpvae_hip.so variants into
 # abl/<variant>/ (here: `build`) and times them on the GPU box (`run`).
-# A variant is <bits>[:<MACRO>=<value>]: <bits> = MPV_ABL (probit_fwd.hip /
-# probit_bwd.hip), the optional macro is passed as -D<MACRO>=<value>.
+# A variant is <bits>[:<extra>...]: <bits> = MPV_ABL (probit_fwd.hip /
+# probit_bwd.hip); each ':'-separated extra is MACRO=value (-D) or a raw -flag.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 VARIANTS="${VARIANTS:-0 1 5 9 17 13 25}"
-dir_of() { echo "$R/abl/$(echo "$1" | tr ':=' '__')"; }
+dir_of() { echo "$R/abl/$(echo "$1" | tr ':=' '__' | tr -d ' ')"; }
 case "$1" in
   build)
     cd "$R/mpvae-1_amd" && make -s >/dev/null || exit 1
     for v in $VARIANTS; do
       d=$(dir_of "$v"); mkdir -p "$d"
       bits=${v%%:*}; extra=""
-      [[ "$v" == *:* ]] && extra="-D${v#*:}"
+      if [[ "$v" == *:* ]]; then   # extras: MACRO=value or a raw -flag, ':'-separated
+        IFS=':' read -ra parts <<< "${v#*:}"
+        for x in "${parts[@]}"; do [[ "$x" == -* ]] && extra="$extra $x" || extra="$extra -D$x"; done
+      fi
       for f in probit_fwd probit_bwd; do
         /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -Icsrc \
           -DMPV_ABL=$bits $extra -c csrc/$f.hip -o "$d/$f.o" &

@@ -42,3 +42,21 @@ for blk in range(2):
         ph = [t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[1:, 0] - t[:-1, 3]]
         print(f"block {blk} wave {w}: " + "  ".join(f"{n} {int(np.median(p))}" for n, p in zip(names, ph))
               + f"  iter {int(np.median(t[1:, 0] - t[:-1, 0]))}")
+
+fn = getattr(lib, "mpv_dbg_fwd_stamps", None)
+if fn is not None:
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
+    fb = np.zeros((2, 4, 32, 4), np.uint64)
+    eb = np.zeros((2, 4, 8, 2), np.uint64)
+    assert fn(fb.ctypes.data, eb.ctypes.data) == 0
+    st, ep = fb.astype(np.int64), eb.astype(np.int64)
+    names = ["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"]
+    for blk in range(2):
+        for w in range(4):
+            t = st[blk, w]
+            ph = [t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[1:, 0] - t[:-1, 3]]
+            e = ep[blk, w]
+            print(f"fwd block {blk} wave {w}: " +
+                  "  ".join(f"{n} {int(np.median(p))}" for n, p in zip(names, ph)) +
+                  f"  iter {int(np.median(t[1:, 0] - t[:-1, 0]))}  epilogue {int(np.median(e[:, 1] - e[:, 0]))}"
+                  f"  tile {int(np.median(e[1:, 0] - e[:-1, 0]))}")
