@@ -50,8 +50,11 @@ struct FwdParams {
 #ifndef MPV_FWD_T
 #define MPV_FWD_T 1
 #endif
-#ifndef MPV_FWD_SCALAR
-#define MPV_FWD_SCALAR 0
+#ifndef MPV_FWD_SPREAD
+#define MPV_FWD_SPREAD 0
+#endif
+#ifndef MPV_FWD_WIDE
+#define MPV_FWD_WIDE 1
 #endif
 
 // In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
@@ -159,6 +162,19 @@ MPV_DEV void fwd_cols_stage(float* cols, const FwdParams& p, int b, int n0, int 
     const int64_t o = (int64_t)b * p.L + (ok ? col : 0);
     cols[i] = ok ? p.fe[o] : 0.0f;
     cols[BN + i] = ok ? p.fx[o] : 0.0f;
+    cols[2 * BN + i] = ok ? p.y[o] : 0.0f;
+  }
+}
+
+// The transposed kernel's layout: colsT[2*BN] = (fe, fx) pairs, then y[BN].
+template <int BN>
+MPV_DEV void fwd_cols_stage_t(float* cols, const FwdParams& p, int b, int n0, int nthreads) {
+  for (int i = threadIdx.x; i < BN; i += nthreads) {
+    const int col = n0 + i;
+    const bool ok = col < p.L;
+    const int64_t o = (int64_t)b * p.L + (ok ? col : 0);
+    cols[2 * i] = ok ? p.fe[o] : 0.0f;
+    cols[2 * i + 1] = ok ? p.fx[o] : 0.0f;
     cols[2 * BN + i] = ok ? p.y[o] : 0.0f;
   }
 }
@@ -515,6 +531,27 @@ struct Fwd16Dma {
       if (++tile < tile_end) set_tile(p, b);
     }
   }
+
+  // The same stage split up: piece i (0 .. JA+JB-1) of the current stage, then
+  // advance() once all of them are issued (spreads the DMA over the MFMAs).
+  MPV_DEV bool active(int tile_end) const { return tile < tile_end; }
+  MPV_DEV void piece_i(int i, char* dst) {
+    const int kb = kc * kRowB;
+    if (i < JA) {
+      const int pc = wid + i * NW;
+      if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[i], dst + pc * 1024);
+    } else {
+      const int pc = wid + (i - JA) * NW;
+      if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[i - JA], dst + BM * kRowB + pc * 1024);
+    }
+  }
+  MPV_DEV void advance(const FwdParams& p, int tile_end, int nK, int b) {
+    ++issued;
+    if (++kc == nK) {
+      kc = 0;
+      if (++tile < tile_end) set_tile(p, b);
+    }
+  }
 };
 
 // Operand fragments of one K stage: A (eps rows) and B (R rows), hi and lo.
@@ -678,6 +715,32 @@ MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int ws, int
   }
 }
 
+// MFMAs of one stage with the DMA pieces of the next stage spread between
+// them (one piece per SPREAD (label, sample) tile pairs), so the stream never
+// stalls this wave for long on a busy address unit.
+template <int TL, int TS, int NPIECE, class Dma>
+MPV_DEV void fwd16t_mfma_dma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f, Dma& dma, bool dmaon,
+                             char* dst) {
+  constexpr int SPREAD = (TL * TS) / NPIECE > 0 ? (TL * TS) / NPIECE : 1;
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < TS; ++n) {
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
+                                                         acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
+                                                         acc[m][n], 0, 0, 0);
+      const int pi = m * TS + n;
+      if (pi % SPREAD == SPREAD - 1 && pi / SPREAD < NPIECE) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (dmaon) dma.piece_i(pi / SPREAD, dst);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+}
+
 template <int TL, int TS>
 MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
 #pragma unroll
@@ -709,6 +772,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   f32x2 sl[TS], sp[TS], sn[TS];  // per sample: log-prob, P, N (label .x / feature .y branch)
 #pragma unroll
   for (int n = 0; n < TS; ++n) sl[n] = sp[n] = sn[n] = splat2(0.0f);
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < TS; ++n) acc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
   // T stash first, all label groups of a sample back to back: the 4 lane rows
   // x TL groups cover whole 128-B lines of the sample's T row (written while
   // still combinable in L2, rather than as half lines far apart in time)
@@ -722,7 +789,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
         for (int m = 0; m < TL; ++m) {
           const int lb = (wl * TL + m) * 16 + lg * 4;
-          const f32x4 t4 = acc[m][n] * scale;
+          const f32x4 t4 = acc[m][n];
           if (vecT && n0 + lb + 3 < L) {
             *reinterpret_cast<f32x4*>(row + lb) = t4;
           } else {
@@ -746,81 +813,46 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + 1][n];
     const int lb = (wl * TL + m) * 16 + lg * 4;  // first of the lane's 4 labels in the tile
-    const f32x4 fe4 = *reinterpret_cast<const f32x4*>(cols + lb);
-    const f32x4 fx4 = *reinterpret_cast<const f32x4*>(cols + BN + lb);
+    const f32x4 pa = *reinterpret_cast<const f32x4*>(cols + 2 * lb);  // (fe, fx) of labels 0, 1
+    const f32x4 pb = *reinterpret_cast<const f32x4*>(cols + 2 * lb + 4);  // labels 2, 3
+    const f32x2 fex[4] = {f32x2{pa[0], pa[1]}, f32x2{pa[2], pa[3]}, f32x2{pb[0], pb[1]},
+                          f32x2{pb[2], pb[3]}};
     const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
-    float wok[4], wpos[4], wneg[4], sg[4];
+    // per label: weights (valid / positive / negative), ranking exponent scale,
+    // and q = qa * E + qb selecting E (y = 1) or 1 - E (y = 0) without a select
+    float wok[4], wpos[4], wneg[4], sg[4], qa[4], qb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       wok[i] = n0 + lb + i < L ? 1.0f : 0.0f;
       wpos[i] = y4[i] == 1.0f ? wok[i] : 0.0f;
       wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
       sg[i] = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
+      qa[i] = y4[i] == 0.0f ? -1.0f : 1.0f;
+      qb[i] = y4[i] == 0.0f ? 1.0f : 0.0f;
     }
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
       const int s = s0 + (ws * TS + n) * 16 + lr;
-      const bool rowok = s >= s_own && s < S;
-      const float wr = rowok ? 1.0f : 0.0f;
-      const f32x4 t4 = am[n] * scale;
-#if MPV_FWD_SCALAR
-      // scalar path: 8 probits (4 labels x 2 branches) in lockstep
-      float u8[8], E8[8];
+      const float wr = (s >= s_own && s < S) ? 1.0f : 0.0f;
+      const f32x4 t4 = am[n];
+      f32x2 uu[4], E4[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        u8[2 * i] = t4[i] + fe4[i];
-        u8[2 * i + 1] = t4[i] + fx4[i];
-      }
-      probit_probN<8>(u8, E8);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float y = y4[i];
-        float le, lx;
-        if (y == 0.0f) {
-          le = fast_log(1.0f - E8[2 * i]);
-          lx = fast_log(1.0f - E8[2 * i + 1]);
-        } else {
-          le = fast_log(E8[2 * i]);
-          lx = fast_log(E8[2 * i + 1]);
-        }
-        if (soft_any && !(y == 0.0f || y == 1.0f)) {
-          le = y * fast_log(E8[2 * i]) + (1.0f - y) * fast_log(1.0f - E8[2 * i]);
-          lx = y * fast_log(E8[2 * i + 1]) + (1.0f - y) * fast_log(1.0f - E8[2 * i + 1]);
-        }
-        const float re = __builtin_amdgcn_exp2f(E8[2 * i] * sg[i]);
-        const float rx = __builtin_amdgcn_exp2f(E8[2 * i + 1] * sg[i]);
-        const float wo = wr * wok[i], wp = wr * wpos[i], wq = wr * wneg[i];
-        sl[n].x = fmaf(wo, le, sl[n].x);
-        sl[n].y = fmaf(wo, lx, sl[n].y);
-        sp[n].x = fmaf(wp, re, sp[n].x);
-        sp[n].y = fmaf(wp, rx, sp[n].y);
-        sn[n].x = fmaf(wq, re, sn[n].x);
-        sn[n].y = fmaf(wq, rx, sn[n].y);
-        ce[i].x = fmaf(wr, E8[2 * i], ce[i].x);
-        ce[i].y = fmaf(wr, E8[2 * i + 1], ce[i].y);
-      }
-#else
-      f32x2 uu[4], E4[4], phi4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + f32x2{fe4[i], fx4[i]};
+      for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + fex[i];
       if (MPV_ABL & 4096) {  // timing study: no probit
 #pragma unroll
         for (int i = 0; i < 4; ++i) E4[i] = uu[i] * 0.01f + splat2(0.5f);
       } else {
-        probit_eval2xN<4>(uu, E4, phi4);
+        probit_prob2xN<4>(uu, E4);
       }
-      f32x2 lp[4], r[4];
+      f32x2 lp[4], r[4];  // lp in log2 units (ln 2 is applied once per sample)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const f32x2 E = E4[i];
-        const float y = y4[i];
         // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
-        const f32x2 q = (y == 0.0f) ? splat2(1.0f) - E : E;
-        lp[i] = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)} *
-                0.6931471805599453f;
+        const f32x2 q = pk_fma(E4[i], splat2(qa[i]), splat2(qb[i]));
+        lp[i] = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)};
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-        const f32x2 a = E * sg[i];
+        const f32x2 a = E4[i] * sg[i];
         r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       }
       if (soft_any) {
@@ -829,19 +861,19 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
           const float y = y4[i];
           if (!(y == 0.0f || y == 1.0f)) {
             const f32x2 E = E4[i];
-            lp[i].x = y * fast_log(E.x) + (1.0f - y) * fast_log(1.0f - E.x);
-            lp[i].y = y * fast_log(E.y) + (1.0f - y) * fast_log(1.0f - E.y);
+            lp[i].x = y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
+            lp[i].y = y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
           }
         }
       }
+      // row sums need no validity weight: only the tile's own rows are published
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sl[n] = pk_fma(splat2(wr * wok[i]), lp[i], sl[n]);
-        sp[n] = pk_fma(splat2(wr * wpos[i]), r[i], sp[n]);
-        sn[n] = pk_fma(splat2(wr * wneg[i]), r[i], sn[n]);
+        sl[n] = pk_fma(splat2(wok[i]), lp[i], sl[n]);
+        sp[n] = pk_fma(splat2(wpos[i]), r[i], sp[n]);
+        sn[n] = pk_fma(splat2(wneg[i]), r[i], sn[n]);
         ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
       }
-#endif
       __builtin_amdgcn_sched_barrier(0);  // one sample at a time: bounded live ranges
     }
     // column sums of these 4 labels over the wave's samples: 16-lane trees,
@@ -864,6 +896,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // row statistics: sum over the 4 lane rows; lanes of row 0 publish
 #pragma unroll
   for (int n = 0; n < TS; ++n) {
+    sl[n] = sl[n] * 0.6931471805599453f;  // rows outside the tile's own range are not published
     const float v[6] = {sl[n].x, sl[n].y, sp[n].x, sn[n].x, sp[n].y, sn[n].y};
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -888,7 +921,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 }
 
 template <int WL, int WS, int TL, int TS, int NSTAGE>
-__global__ __launch_bounds__(WL* WS * 64, 2) void probit_fwd16t_kernel(FwdParams p) {
+__global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
   constexpr int NW = WL * WS;
   constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
   constexpr int STAGE = (BM + BN) * kRowB;
@@ -913,7 +946,7 @@ __global__ __launch_bounds__(WL* WS * 64, 2) void probit_fwd16t_kernel(FwdParams
   const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
   const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
 
-  fwd_cols_stage<BN>(cols, p, b, n0, NW * 64);
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
   for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
   // does the label tile hold soft (non 0/1) labels?  (uniform; enables the
   // two-log BCE path of the epilogue)
@@ -940,7 +973,7 @@ __global__ __launch_bounds__(WL* WS * 64, 2) void probit_fwd16t_kernel(FwdParams
 #pragma unroll
       for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int kc = 0; kc < nK; ++kc, ++gs) {
+    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
       FWD_STAMP(0);
       if (NSTAGE == 2)
         wait_vmcnt<0>();
@@ -950,15 +983,32 @@ __global__ __launch_bounds__(WL* WS * 64, 2) void probit_fwd16t_kernel(FwdParams
       FWD_STAMP(1);
       barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
       FWD_STAMP(2);
-      dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
-      FWD_STAMP(3);
       FragT<TL, TS> f;
-      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
-      fwd16t_mfma<TL, TS>(acc, f);
+      if (MPV_FWD_SPREAD) {
+        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
+        const bool dmaon = dma.active(t_end);
+        fwd16t_mfma_dma<TL, TS, Fwd16Dma<BM, BN, NW>::JA + Fwd16Dma<BM, BN, NW>::JB>(
+            acc, f, dma, dmaon, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
+        if (dmaon) dma.advance(p, t_end, nK, b);
+      } else {
+        dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+        FWD_STAMP(3);
+        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
+        fwd16t_mfma<TL, TS>(acc, f);
+      }
     }
     FWD_ESTAMP(0);
-    fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                        soft_any);
+    if (MPV_ABL & 1) {  // timing study: no epilogue
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
+    } else {
+      fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                          soft_any);
+    }
     FWD_ESTAMP(1);
   }
   // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
@@ -1090,11 +1140,12 @@ struct FwdPlan {
   size_t rowpart_bytes, colpart_bytes;
 };
 
-static FwdPlan plan_fwd(const mpv_shape* s) {
+static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
-  pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : 2);
+  const bool wide = MPV_FWD_WIDE && gemm == MPV_GEMM_F16X3 && s->L > 128;
+  pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : (wide ? 3 : 2));
   pl.BM = 128;
-  pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : 128);
+  pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
   // enough workgroups to fill 256 CUs several times; fewer s-chunks = fewer partials
@@ -1128,6 +1179,9 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         break;
       case 1:  // BN 96, 8 waves, 4-stage ring (112 KB)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
+        break;
+      case 3:  // 256 labels x 128 samples, 8 waves of 64 x 64, one workgroup per CU
+        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, 2>), grid, dim3(512), 0, st, p);
         break;
       default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
         if (MPV_FWD_T) {
@@ -1171,8 +1225,12 @@ int mpv_dbg_fwd_stamps(void* host_out, void* host_epi) {
 
 size_t mpv_fwd_workspace_bytes(const mpv_shape* shape) {
   if (check_shape(shape) != MPV_OK) return 0;
-  const FwdPlan pl = plan_fwd(shape);
-  return pl.rowpart_bytes + pl.colpart_bytes;
+  size_t most = 0;  // enough for either GEMM mode's tiling
+  for (int gemm : {MPV_GEMM_F16X3, MPV_GEMM_F32}) {
+    const FwdPlan pl = plan_fwd(shape, gemm);
+    most = std::max(most, pl.rowpart_bytes + pl.colpart_bytes);
+  }
+  return most;
 }
 
 int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) {
@@ -1183,7 +1241,7 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
               "NULL pointer in mpv_fwd_args");
   MPV_REQUIRE(a->gemm == MPV_GEMM_F32 || a->gemm == MPV_GEMM_F16X3, "unknown gemm mode %d",
               a->gemm);
-  const FwdPlan pl = plan_fwd(shape);
+  const FwdPlan pl = plan_fwd(shape, a->gemm);
   if (a->gemm == MPV_GEMM_F32) {
     MPV_REQUIRE(a->R32 && a->eps, "MPV_GEMM_F32 needs R32 and eps");
   } else {

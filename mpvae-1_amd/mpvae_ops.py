@@ -107,7 +107,7 @@ class HipShardBackend:
             return self.to_f32(R)
         L, z = R.shape
         return self._split(R.detach().contiguous(), L, z,
-                           Planes(_pad(L, 128), _pad(z, 128), R.device))
+                           Planes(_pad(L, 256), _pad(z, 128), R.device))
 
     def to_f32(self, R):
         if R.dtype == torch.float32:

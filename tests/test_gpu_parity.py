@@ -114,7 +114,7 @@ def test_split_planes_round_trip():
     for scale in (1e-6, 0.05, 3.0, 2e4):
         R = torch.randn((37, 53), device=DEV, dtype=torch.float64, generator=g) * scale
         pl = be.prepare_R(R)
-        assert pl.rows_pad == 128 and pl.cols == 128 and pl.ld == 256
+        assert pl.rows_pad == 256 and pl.cols == 128 and pl.ld == 256
         v = pl.value().double()
         err = (v[:37, :53] - R).abs().max() / R.abs().max()
         assert float(err) < 1e-6, (scale, float(err))

@@ -2,7 +2,7 @@
 # SQ/TCC counter passes (one rocprofv3 --pmc run per set) on the bench workload.
 # Usage on the GPU box: SETS="A B" bash tools/counters.sh ; results in gpurun_out/ctr/
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-OUT="$R/gpurun_out/ctr"
+OUT="${CTR_OUT:-$R/gpurun_out/ctr}"
 ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}"
 KRE="${KRE:-probit_fwd|dR16|dR_gemm|bwd_elem|noise}"
 mkdir -p "$OUT"
