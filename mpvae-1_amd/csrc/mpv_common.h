@@ -186,6 +186,43 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
   }
 }
 
+// probit_eval2xN for the backward, with the forward's folded constants
+// (probit_prob2xN): E and phic = (1 - 1e-6) phi(u), the factor dE/du needs.
+// erfc = t * exp(-z^2) * exp(P(t)): exp(-z^2) also gives phi.
+template <int N>
+MPV_DEV void probit_dE2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phic)[N]) {
+#pragma clang fp contract(off)
+  constexpr float kL2e = 1.4426950408889634f, kSqL2e = 1.2011224087864498f;
+  constexpr float c[10] = {0.17087277f * kL2e, -0.82215223f * kL2e, 1.48851587f * kL2e,
+                           -1.13520398f * kL2e, 0.27886807f * kL2e, -0.18628806f * kL2e,
+                           0.09678418f * kL2e, 0.37409196f * kL2e, 1.00002368f * kL2e,
+                           -1.26551223f * kL2e};
+  f32x2 zq[N], t[N], p[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    zq[j] = f32x2{fabsf(u[j].x), fabsf(u[j].y)} * (kInvSqrt2 * kSqL2e);
+    const f32x2 den = pk_fma(splat2(0.5f / kSqL2e), zq[j], splat2(1.0f));
+    t[j] = f32x2{fast_rcp(den.x), fast_rcp(den.y)};
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
+#pragma unroll
+  for (int k = 2; k < 10; ++k)
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], p[j], splat2(c[k]));
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const f32x2 az = -zq[j] * zq[j];
+    const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
+    const f32x2 ep = f32x2{__builtin_amdgcn_exp2f(p[j].x), __builtin_amdgcn_exp2f(p[j].y)};
+    phic[j] = ez * (kC1 * kInvSqrt2Pi);
+    const f32x2 om = splat2(1.0f) - (t[j] * ez) * ep;
+    const f32x2 onep = splat2(1.0f) + f32x2{__builtin_copysignf(om.x, u[j].x),
+                                            __builtin_copysignf(om.y, u[j].y)};
+    E[j] = onep * (0.5f * kC1) + splat2(kC0);
+  }
+}
+
 // Scalar lockstep version (N independent evaluations, no packed ops):
 // bit-identical to N probit_eval calls (phi omitted).
 template <int N>

@@ -117,6 +117,7 @@ struct ElemCol {
   float y[4];
   bool soft[4];
   float sdl[4];   // sign of d logp/dE for a 0/1 label: -1 for y = 0, +1 otherwise
+  float qa[4], qb[4];  // d = qa E + qb: 1 - E for y = 0, E otherwise
   float sgx[4];   // e^{-5E} (y = 1) or e^{5E}: exponent multiplier in log2 units
   float wp[4], wn[4];  // [y = 1], [y = 0]
 };
@@ -125,14 +126,16 @@ struct ElemCol {
 // dependent packed ops of one element interleave with the others'.
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
                        f32x2 (&out)[4]) {
-  f32x2 u[4], E[4], phi[4];
+  f32x2 u[4], E[4], phic[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + c.base[q];
-  probit_eval2xN<4>(u, E, phi);
+  probit_dE2xN<4>(u, E, phic);
+  const f32x2 nbP = -bP;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    // d logp / dE = y/E - (1-y)/(1-E): one reciprocal for a 0/1 label
-    const f32x2 d = (c.y[q] == 0.0f) ? splat2(1.0f) - E[q] : E[q];
+    // d logp / dE = y/E - (1-y)/(1-E): one reciprocal of E (y = 1) or 1 - E
+    // (y = 0), selected as qa E + qb
+    const f32x2 d = pk_fma(E[q], splat2(c.qa[q]), splat2(c.qb[q]));
     const f32x2 r = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
     f32x2 dE;
     if (c.soft[q]) {
@@ -143,10 +146,10 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
       dE = pk_fma(alpha * c.sdl[q], r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-    const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(-c.wp[q]) * bP);
+    const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP);
     const f32x2 a = E[q] * c.sgx[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
-    out[q] = (dE * kC1) * phi[q];
+    out[q] = dE * phic[q];
   }
   // a degenerate row poisons every label, whatever its value (reference autograd)
   if (bP.x != bP.x || bP.y != bP.y) {
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     gil[q] = (ok[q] && p.gIL) ? p.gIL[o] * p.inv_S : 0.0f;
     soft[q] = !(yv[q] == 0.0f || yv[q] == 1.0f);
   }
-  float se[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x2 sg2[4] = {splat2(0.f), splat2(0.f), splat2(0.f), splat2(0.f)};  // (label, feature)
   ElemCol ec;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -217,6 +220,8 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     ec.y[q] = yv[q];
     ec.soft[q] = soft[q];
     ec.sdl[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
+    ec.qa[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
+    ec.qb[q] = yv[q] == 0.0f ? 1.0f : 0.0f;
     ec.sgx[q] = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
     ec.wp[q] = yv[q] == 1.0f ? 1.0f : 0.0f;
     ec.wn[q] = yv[q] == 0.0f ? 1.0f : 0.0f;
@@ -241,10 +246,10 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
       } else {
         d_elem2x4(cur.t, ec, cur.alpha, cur.bP, cur.bN, g2);
       }
+      // column sums: pad columns (finite, never published) need no mask
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        se[q] += ok[q] ? g2[q].x : 0.0f;
-        sx[q] += ok[q] ? g2[q].y : 0.0f;
+        sg2[q] = sg2[q] + g2[q];
         G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
       }
       if (PLANES && !(MPV_ABL & 32768)) {
@@ -273,8 +278,8 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   // column sums over this block's rows: reduce the RPI row-lanes per column
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    cred[tid * 8 + q] = se[q];
-    cred[tid * 8 + 4 + q] = sx[q];
+    cred[tid * 8 + q] = sg2[q].x;
+    cred[tid * 8 + 4 + q] = sg2[q].y;
   }
   __syncthreads();
   for (int j = tid; j < p.TPR * 4; j += blockDim.x) {
