@@ -131,6 +131,8 @@ RANDOM_CASES = [
     (200, 64, 5, 257, 8),        # two column tiles, ragged s tiles
     (1024, 1024, 2, 48, 50),     # C4 dims, tiny batch
     (1030, 96, 2, 20, 8),        # L > 1024: two bwd column chunks
+    (1024, 1000, 2, 300, 8),     # pipelined forward epilogue: 3 sample tiles, ragged K
+    (260, 1024, 3, 257, 8),      # pipelined, pad labels in the last label tile
 ]
 
 
