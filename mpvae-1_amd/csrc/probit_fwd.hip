@@ -53,6 +53,9 @@ struct FwdParams {
 #ifndef MPV_FWD_SPREAD
 #define MPV_FWD_SPREAD 0
 #endif
+#ifndef MPV_FWD_PRIO
+#define MPV_FWD_PRIO 1
+#endif
 #ifndef MPV_FWD_WIDE
 #define MPV_FWD_WIDE 1
 #endif
@@ -60,8 +63,8 @@ struct FwdParams {
 // In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
 // points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
 #if (MPV_ABL & 1024)
-__device__ unsigned long long g_fwd_stamps[2][4][32][4];
-__device__ unsigned long long g_fwd_epi[2][4][8][2];
+__device__ unsigned long long g_fwd_stamps[2][8][32][4];
+__device__ unsigned long long g_fwd_epi[2][8][8][2];
 #define FWD_STAMP(k)                                                                  \
   do {                                                                                \
     if (blockIdx.x < 2 && gs >= 256 && gs < 288 && (threadIdx.x & 63) == 0)           \
@@ -965,6 +968,9 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
 
   int gs = 0;
+  // the second half of the waves loses every age arbitration on its SIMD;
+  // static priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (MPV_FWD_PRIO && wid >= NW / 2) __builtin_amdgcn_s_setprio(MPV_FWD_PRIO);
   for (int st = t_begin; st < t_end; ++st) {
     const int s0 = fwd_tile_s0<BM>(st, p.S);
     f32x4 acc[TL][TS];

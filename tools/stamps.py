@@ -24,6 +24,7 @@ args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=
                           nll_coeff=nllc, c_coeff=cc, mpvae_noise="philox", mpvae_shard=False,
                           mpvae_gemm="f16x3")
 y, leaves = bench.make_inputs(L, z, B, d, dev)
+print("stepping", flush=True)
 for it in range(2):
     bench.step(y, leaves, args, it)
 torch.cuda.synchronize()
@@ -46,13 +47,13 @@ for blk in range(2):
 fn = getattr(lib, "mpv_dbg_fwd_stamps", None)
 if fn is not None:
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
-    fb = np.zeros((2, 4, 32, 4), np.uint64)
-    eb = np.zeros((2, 4, 8, 2), np.uint64)
+    fb = np.zeros((2, 8, 32, 4), np.uint64)
+    eb = np.zeros((2, 8, 8, 2), np.uint64)
     assert fn(fb.ctypes.data, eb.ctypes.data) == 0
     st, ep = fb.astype(np.int64), eb.astype(np.int64)
     names = ["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"]
     for blk in range(2):
-        for w in range(4):
+        for w in range(8):
             t = st[blk, w]
             ph = [t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2], t[1:, 0] - t[:-1, 3]]
             e = ep[blk, w]
