@@ -59,6 +59,25 @@ struct FwdParams {
 #ifndef MPV_FWD_WIDE
 #define MPV_FWD_WIDE 1
 #endif
+// Start-phase stagger of co-resident workgroups (study): mode 1 delays blocks
+// [256, 512), mode 2 odd blocks, mode 3 blocks with (b >> 3) odd, by
+// MPV_FWD_STAG_N x s_sleep 127 (~8k cycles each) before the first DMA.
+// Which waves of the 8-wave transposed kernel issue the stage DMA: 0 all,
+// 1 waves NW/2.. (the prio-1 half), 2 waves 0..NW/2-1.  With one half issuing,
+// the other half starts its MFMAs right after the barrier.
+#ifndef MPV_FWD_DMAW
+#define MPV_FWD_DMAW 1
+#endif
+// 256 x 256 tiles (8 waves of 128 labels x 64 samples) for the wide f16x3 case
+#ifndef MPV_FWD_BIG
+#define MPV_FWD_BIG 0
+#endif
+#ifndef MPV_FWD_STAG_MODE
+#define MPV_FWD_STAG_MODE 0
+#endif
+#ifndef MPV_FWD_STAG_N
+#define MPV_FWD_STAG_N 8
+#endif
 
 // In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
 // points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
@@ -830,8 +849,11 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       wpos[i] = y4[i] == 1.0f ? wok[i] : 0.0f;
       wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
       sg[i] = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
-      qa[i] = y4[i] == 0.0f ? -1.0f : 1.0f;
-      qb[i] = y4[i] == 0.0f ? 1.0f : 0.0f;
+      // q = qa * E + qb: E (y = 1), 1 - E (y = 0), 1 (pad label or soft label,
+      // whose two-log BCE term is added separately)
+      const bool hard = wok[i] != 0.0f && (y4[i] == 0.0f || y4[i] == 1.0f);
+      qa[i] = !hard ? 0.0f : (y4[i] == 0.0f ? -1.0f : 1.0f);
+      qb[i] = !hard ? 1.0f : (y4[i] == 0.0f ? 1.0f : 0.0f);
     }
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
@@ -848,31 +870,35 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       } else {
         probit_prob2xN<4>(uu, E4);
       }
-      f32x2 lp[4], r[4];  // lp in log2 units (ln 2 is applied once per sample)
+      f32x2 q[4], r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        // BCE log-prob (mpvae.py:184-185): one log for a 0/1 label
-        const f32x2 q = pk_fma(E4[i], splat2(qa[i]), splat2(qb[i]));
-        lp[i] = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)};
+        // BCE operand (mpvae.py:184-185): E for y = 1, 1 - E for y = 0, 1 for a pad label
+        q[i] = pk_fma(E4[i], splat2(qa[i]), splat2(qb[i]));
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
         const f32x2 a = E4[i] * sg[i];
         r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       }
+      // sum of the 4 labels' log-probs as ONE log of their product (log2 units,
+      // ln 2 applied once per sample): every q >= 4.7e-7 (the delta clamp), so
+      // the product of 4 stays >= 5e-26, far from underflow
+      const f32x2 q4 = (q[0] * q[1]) * (q[2] * q[3]);
+      f32x2 lp = f32x2{__builtin_amdgcn_logf(q4.x), __builtin_amdgcn_logf(q4.y)};
       if (soft_any) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float y = y4[i];
-          if (!(y == 0.0f || y == 1.0f)) {
+          if (wok[i] != 0.0f && !(y == 0.0f || y == 1.0f)) {  // soft label: both BCE terms (q = 1)
             const f32x2 E = E4[i];
-            lp[i].x = y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
-            lp[i].y = y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
+            lp.x += y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
+            lp.y += y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
           }
         }
       }
       // row sums need no validity weight: only the tile's own rows are published
+      sl[n] = sl[n] + lp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sl[n] = pk_fma(splat2(wok[i]), lp[i], sl[n]);
         sp[n] = pk_fma(splat2(wpos[i]), r[i], sp[n]);
         sn[n] = pk_fma(splat2(wneg[i]), r[i], sn[n]);
         ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
@@ -941,6 +967,14 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = wid % WL, ws = wid / WL;
+  if (MPV_FWD_STAG_MODE) {
+    const unsigned bi = blockIdx.x;
+    const bool late = MPV_FWD_STAG_MODE == 1 ? (bi >= 256 && bi < 512)
+                      : MPV_FWD_STAG_MODE == 2 ? (bi < 512 && (bi & 1) != 0)
+                                               : (bi < 512 && ((bi >> 3) & 1) != 0);
+    if (late)
+      for (int i = 0; i < MPV_FWD_STAG_N; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int lr = lane & 15, lg = lane >> 4;
 
   const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
@@ -962,10 +996,14 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
     }
   }
   const bool soft_any = __syncthreads_or(my_soft);
-  Fwd16Dma<BM, BN, NW> dma;
-  dma.init(p, t_begin, b, n0, wid, lane);
+  constexpr int NWD = MPV_FWD_DMAW ? NW / 2 : NW;  // DMA-issuing waves
+  const bool dmaw = MPV_FWD_DMAW == 0 || ((MPV_FWD_DMAW == 1) == (wid >= NW / 2));
+  Fwd16Dma<BM, BN, NWD> dma;
+  dma.init(p, t_begin, b, n0, MPV_FWD_DMAW == 1 ? wid - NW / 2 : wid % NWD, lane);
+  if (dmaw) {
 #pragma unroll
-  for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
 
   int gs = 0;
   // the second half of the waves loses every age arbitration on its SIMD;
@@ -993,11 +1031,11 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
       if (MPV_FWD_SPREAD) {
         fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
         const bool dmaon = dma.active(t_end);
-        fwd16t_mfma_dma<TL, TS, Fwd16Dma<BM, BN, NW>::JA + Fwd16Dma<BM, BN, NW>::JB>(
+        fwd16t_mfma_dma<TL, TS, Fwd16Dma<BM, BN, NWD>::JA + Fwd16Dma<BM, BN, NWD>::JB>(
             acc, f, dma, dmaon, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
         if (dmaon) dma.advance(p, t_end, nK, b);
       } else {
-        dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+        if (dmaw) dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
         FWD_STAMP(3);
         fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
         fwd16t_mfma<TL, TS>(acc, f);
@@ -1150,7 +1188,7 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
   const bool wide = MPV_FWD_WIDE && gemm == MPV_GEMM_F16X3 && s->L > 128;
   pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : (wide ? 3 : 2));
-  pl.BM = 128;
+  pl.BM = (pl.cfg == 3 && MPV_FWD_BIG) ? 256 : 128;
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
@@ -1187,7 +1225,10 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
         break;
       case 3:  // 256 labels x 128 samples, 8 waves of 64 x 64, one workgroup per CU
-        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, 2>), grid, dim3(512), 0, st, p);
+        if (MPV_FWD_BIG)  // 256 labels x 256 samples, 8 waves of 128 x 64
+          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
+        else
+          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, 2>), grid, dim3(512), 0, st, p);
         break;
       default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
         if (MPV_FWD_T) {
