@@ -72,6 +72,17 @@ struct FwdParams {
 #ifndef MPV_FWD_BIG
 #define MPV_FWD_BIG 0
 #endif
+// epilogue study knobs: priority of every wave during the epilogue (-1: keep
+// the K-loop priorities), nontemporal T stores
+#ifndef MPV_EPI_PRIO
+#define MPV_EPI_PRIO 0
+#endif
+#ifndef MPV_T_NT
+#define MPV_T_NT 0
+#endif
+#ifndef MPV_EPI_SB
+#define MPV_EPI_SB 4
+#endif
 #ifndef MPV_FWD_STAG_MODE
 #define MPV_FWD_STAG_MODE 0
 #endif
@@ -83,7 +94,7 @@ struct FwdParams {
 // points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
 #if (MPV_ABL & 1024)
 __device__ unsigned long long g_fwd_stamps[2][8][32][4];
-__device__ unsigned long long g_fwd_epi[2][8][8][2];
+__device__ unsigned long long g_fwd_epi[2][8][8][6];
 #define FWD_STAMP(k)                                                                  \
   do {                                                                                \
     if (blockIdx.x < 2 && gs >= 256 && gs < 288 && (threadIdx.x & 63) == 0)           \
@@ -94,12 +105,20 @@ __device__ unsigned long long g_fwd_epi[2][8][8][2];
     if (blockIdx.x < 2 && st - t_begin >= 8 && st - t_begin < 16 && (threadIdx.x & 63) == 0) \
       g_fwd_epi[blockIdx.x][threadIdx.x >> 6][st - t_begin - 8][k] = __builtin_readcyclecounter(); \
   } while (0)
+#define FWD_ESTAMP2(k)                                                                \
+  do {                                                                                \
+    if (blockIdx.x < 2 && eidx >= 8 && eidx < 16 && (threadIdx.x & 63) == 0)         \
+      g_fwd_epi[blockIdx.x][threadIdx.x >> 6][eidx - 8][k] = __builtin_readcyclecounter(); \
+  } while (0)
 #else
 #define FWD_STAMP(k) \
   do {               \
   } while (0)
 #define FWD_ESTAMP(k) \
   do {                \
+  } while (0)
+#define FWD_ESTAMP2(k) \
+  do {                 \
   } while (0)
 #endif
 
@@ -786,7 +805,7 @@ MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
 template <int WL, int WS, int TL, int TS>
 MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
                                  int b, int s0, int s_own, int nt, float* red, float* cacc,
-                                 const float* cols, bool soft_any) {
+                                 const float* cols, bool soft_any, int eidx) {
   constexpr int NT = WL * WS * 64, BM = WS * TS * 16, BN = WL * TL * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wl = wid % WL, ws = wid / WL, lr = lane & 15, lg = lane >> 4;
@@ -813,7 +832,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
           const int lb = (wl * TL + m) * 16 + lg * 4;
           const f32x4 t4 = acc[m][n];
           if (vecT && n0 + lb + 3 < L) {
-            *reinterpret_cast<f32x4*>(row + lb) = t4;
+            if (MPV_T_NT)
+              __builtin_nontemporal_store(t4, reinterpret_cast<f32x4*>(row + lb));
+            else
+              *reinterpret_cast<f32x4*>(row + lb) = t4;
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -823,6 +845,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       }
     }
   }
+  FWD_ESTAMP2(1);
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
 #pragma unroll 1
@@ -903,7 +926,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         sn[n] = pk_fma(splat2(wneg[i]), r[i], sn[n]);
         ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
       }
-      __builtin_amdgcn_sched_barrier(0);  // one sample at a time: bounded live ranges
+      // MPV_EPI_SB samples at a time: bounded live ranges vs more independent chains
+      if (MPV_EPI_SB > 0 && (n + 1) % MPV_EPI_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
     // column sums of these 4 labels over the wave's samples: 16-lane trees,
     // lane 15 of each row accumulates into the (ws, label) slot it owns
@@ -922,6 +946,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
   }
+  FWD_ESTAMP2(2);
   // row statistics: sum over the 4 lane rows; lanes of row 0 publish
 #pragma unroll
   for (int n = 0; n < TS; ++n) {
@@ -933,6 +958,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       if (lg == 0) red[(wl * BM + (ws * TS + n) * 16 + lr) * 6 + k] = tot;
     }
   }
+  FWD_ESTAMP2(3);
   lds_barrier();
   for (int r = tid; r < BM; r += NT) {
     const int s = s0 + r;
@@ -946,6 +972,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       }
     }
   }
+  FWD_ESTAMP2(4);
   lds_barrier();
 }
 
@@ -1050,10 +1077,17 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
         for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
       p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
     } else {
+      if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
       fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                          soft_any);
+                                          soft_any, st - t_begin);
+      if (MPV_EPI_PRIO >= 0) {  // back to the K-loop priorities
+        if (MPV_FWD_PRIO && wid >= NW / 2)
+          __builtin_amdgcn_s_setprio(MPV_FWD_PRIO);
+        else
+          __builtin_amdgcn_s_setprio(0);
+      }
     }
-    FWD_ESTAMP(1);
+    FWD_ESTAMP(5);
   }
   // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
   lds_barrier();

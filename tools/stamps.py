@@ -48,10 +48,12 @@ fn = getattr(lib, "mpv_dbg_fwd_stamps", None)
 if fn is not None:
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]
     fb = np.zeros((2, 8, 32, 4), np.uint64)
-    eb = np.zeros((2, 8, 8, 2), np.uint64)
+    eb = np.zeros((2, 8, 8, 6), np.uint64)
     assert fn(fb.ctypes.data, eb.ctypes.data) == 0
     st, ep = fb.astype(np.int64), eb.astype(np.int64)
+    np.savez(os.path.join(ROOT, "gpurun_out", "stamps_raw.npz"), fwd=st, epi=ep)
     names = ["wait(vmcnt)", "barrier", "dma issue", "reads+mfma issue"]
+    enames = ["T store", "label loop", "row sums", "rowpart", "tail"]
     for blk in range(2):
         for w in range(8):
             t = st[blk, w]
@@ -59,5 +61,6 @@ if fn is not None:
             e = ep[blk, w]
             print(f"fwd block {blk} wave {w}: " +
                   "  ".join(f"{n} {int(np.median(p))}" for n, p in zip(names, ph)) +
-                  f"  iter {int(np.median(t[1:, 0] - t[:-1, 0]))}  epilogue {int(np.median(e[:, 1] - e[:, 0]))}"
-                  f"  tile {int(np.median(e[1:, 0] - e[:-1, 0]))}")
+                  f"  iter {int(np.median(t[1:, 0] - t[:-1, 0]))}  epilogue {int(np.median(e[:, 5] - e[:, 0]))}"
+                  f" [" + " ".join(f"{n} {int(np.median(e[:, k + 1] - e[:, k]))}" for k, n in enumerate(enames)) +
+                  f"]  tile {int(np.median(e[1:, 0] - e[:-1, 0]))}")
