@@ -56,7 +56,9 @@ def setup_dist():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    # MPVAE_FORCE_DIST=1: a process group (and the sample-shard exchange) even
+    # on one rank -- rehearses the RCCL path on a single-GPU box
+    if world > 1 or os.environ.get("MPVAE_FORCE_DIST") == "1":
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
@@ -192,6 +194,7 @@ def main():
     cli = ap.parse_args()
 
     world, rank, local = setup_dist()
+    forced = dist.is_initialized() and world == 1
     if world != cli.gpus:
         log(f"warning: --gpus {cli.gpus} but WORLD_SIZE {world}; using {world}")
     device = torch.device("cuda", local)
@@ -200,8 +203,8 @@ def main():
     S_local = S if scaling == "weak" else S // world
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_total,
                               n_test_sample=S_total, mode="train", nll_coeff=nllc, c_coeff=cc,
-                              mpvae_noise="philox", mpvae_shard=world > 1,
-                              mpvae_gemm=cli.gemm)
+                              mpvae_noise="philox", mpvae_shard=world > 1 or forced,
+                              mpvae_force_exchange=forced, mpvae_gemm=cli.gemm)
     y, leaves = make_inputs(L, z, B, d, device)
     lib = H.load_library()
 
@@ -210,19 +213,19 @@ def main():
     torch.cuda.synchronize()
     lib.mpv_timing_enable(1)
     lib.mpv_timing_reset()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(cli.steps):
         out = step(y, leaves, args, 1000 + it)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lib.mpv_timing_enable(0)
     times = H.kernel_times()
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
@@ -249,7 +252,7 @@ def main():
             "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

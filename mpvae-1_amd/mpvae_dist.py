@@ -58,12 +58,14 @@ def split_samples(n_sample, world, rank):
 
 
 def shard_for(args, n_sample, group=None):
-    """This rank's slice of the sample axis (the whole axis unless args.mpvae_shard)."""
+    """This rank's slice of the sample axis (the whole axis unless args.mpvae_shard).
+    args.mpvae_force_exchange runs the collectives even on a world of one (a
+    rehearsal of the multi-GPU path on a single GPU)."""
     if not getattr(args, "mpvae_shard", False) or not dist.is_available() \
             or not dist.is_initialized():
         return Shard(n_sample, 0, None)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    if world == 1:
+    if world == 1 and not getattr(args, "mpvae_force_exchange", False):
         return Shard(n_sample, 0, None)
     if n_sample < world:
         raise ValueError(f"n_sample={n_sample} cannot be sharded over {world} ranks")
