@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 2
+#define MPV_ABI_VERSION 3
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -249,6 +249,65 @@ int mpv_reparam_bwd(const mpv_reparam_bwd_args* args, void* stream);
 int mpv_timing_enable(int on);
 int mpv_timing_reset(void);
 int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms);
+
+/* ---- Consumers of indiv_prob / indiv_prob_label in the training step ------
+ * (fairness.hip) */
+
+/* Open-addressing table of 0/1 label patterns -> distance, one per target
+ * fair label: replaces label_distances[target].get(''.join(label.astype(str)),
+ * 0.) per batch row (fairsoft_train.py:85-93).  Key = the pattern packed
+ * 64 labels per word (bit j of word w = label 64w+j), W = ceil(L/64) words;
+ * slot = splitmix64-chain hash & (nslots-1), linear probing, used[slot] = 0
+ * ends a probe.  Built once on the host (mpvae_fair.LabelDistanceTable). */
+typedef struct mpv_label_table {
+  const uint64_t* keys; /* nslots * W */
+  const double* vals;   /* nslots */
+  const int32_t* used;  /* nslots */
+  int64_t nslots;       /* a power of two (0: empty table) */
+  int64_t W;
+} mpv_label_table;
+
+/* w[b] = table value of row b's pattern (0 when absent or not 0/1 after
+ * int()); *contributed += #rows with w > 0 (fairsoft_train.py:91-92). */
+int mpv_label_weights(const float* y, int64_t B, int64_t L, const mpv_label_table* table,
+                      double* w, int32_t* contributed, void* stream);
+
+enum mpv_fair_norm { MPV_FAIR_L1 = 1, MPV_FAIR_L2 = 2 };
+
+/* Fairness regulariser (fairsoft_train.py:95-131), fp64 as in the reference:
+ *   W_t = sum_b w[t,b];  m_t = sum_b w[t,b] z[b] / W_t           (if W_t > 0)
+ *   per sensitive group k: W_tk, m_tk likewise                      (if W_tk > 0)
+ *   out = fair_coeff * sum_{z in label_z, feat_z} sum_t sum_k sum_l f(m_tk - m_t)
+ * with f = |.| (l1) or (.)^2 (l2).  Rows are grouped by `gid` (B), `order`
+ * (B) lists them group by group, `goff` (G+1) holds the group offsets.  The
+ * workspace keeps the backward's tables: pass the same one to mpv_fair_bwd. */
+typedef struct mpv_fair_args {
+  const float* label_z;  /* (B, L) indiv_prob_label */
+  const float* feat_z;   /* (B, L) indiv_prob */
+  const double* w;       /* (T, B) */
+  const int32_t* order;  /* (B) */
+  const int32_t* goff;   /* (G + 1) */
+  const int32_t* gid;    /* (B) */
+  int64_t B, L, T, G;
+  int norm;              /* MPV_FAIR_L1 / MPV_FAIR_L2 (else the penalty is 0) */
+  double fair_coeff;
+  double* out;           /* device scalar */
+} mpv_fair_args;
+
+size_t mpv_fair_workspace_bytes(int64_t L, int64_t T, int64_t G);
+int mpv_fair_fwd(const mpv_fair_args* args, void* workspace, size_t workspace_bytes,
+                 void* stream);
+/* g_label_z, g_feat_z (B, L) = *gout x d out / d label_z, feat_z (sgn(0) = 0). */
+int mpv_fair_bwd(const mpv_fair_args* args, const double* gout, float* g_label_z,
+                 float* g_feat_z, void* workspace, size_t workspace_bytes, void* stream);
+
+/* evals.compute_metrics(pred, target, threshold, all_metrics=False)
+ * (evals.py:178-238) on the device: out[8] = [ACC, HA, ebF1, miF1, maF1,
+ * p@1, p@3, p@5].  Top-k ties go to the larger label index. */
+size_t mpv_metrics_workspace_bytes(int64_t B, int64_t L);
+int mpv_train_metrics(const float* pred, const float* target, int64_t B, int64_t L,
+                      float threshold, double* out, void* workspace, size_t workspace_bytes,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -81,6 +81,22 @@ class ReparamBwdArgs(ctypes.Structure):
                 ("gmu_x", vp), ("glogvar_x", vp), ("n_x", ctypes.c_int64)]
 
 
+class LabelTable(ctypes.Structure):
+    """mpv_label_table: packed 0/1 label patterns -> distance (fairness.hip)."""
+    _fields_ = [("keys", vp), ("vals", vp), ("used", vp), ("nslots", ctypes.c_int64),
+                ("W", ctypes.c_int64)]
+
+
+FAIR_L1, FAIR_L2 = 1, 2
+
+
+class FairArgs(ctypes.Structure):
+    _fields_ = [("label_z", vp), ("feat_z", vp), ("w", vp), ("order", vp), ("goff", vp),
+                ("gid", vp), ("B", ctypes.c_int64), ("L", ctypes.c_int64), ("T", ctypes.c_int64),
+                ("G", ctypes.c_int64), ("norm", ctypes.c_int), ("fair_coeff", ctypes.c_double),
+                ("out", vp)]
+
+
 # name -> (restype, argtypes); exactly the symbols of include/mpvae_hip.h
 SIGNATURES = {
     "mpv_abi_version": (ctypes.c_int, []),
@@ -107,6 +123,16 @@ SIGNATURES = {
     "mpv_timing_reset": (ctypes.c_int, []),
     "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_double)]),
+    "mpv_label_weights": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.POINTER(LabelTable), vp, vp, vp]),
+    "mpv_fair_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64,
+                                                   ctypes.c_int64]),
+    "mpv_fair_fwd": (ctypes.c_int, [ctypes.POINTER(FairArgs), vp, ctypes.c_size_t, vp]),
+    "mpv_fair_bwd": (ctypes.c_int, [ctypes.POINTER(FairArgs), vp, vp, vp, vp, ctypes.c_size_t,
+                                    vp]),
+    "mpv_metrics_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64]),
+    "mpv_train_metrics": (ctypes.c_int, [vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_float,
+                                         vp, vp, ctypes.c_size_t, vp]),
 }
 
 _lib = None
@@ -158,7 +184,7 @@ def require_gpu(*tensors):
 
 KERNELS = ["noise_philox", "split", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
            "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
-           "kl_bwd"]
+           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics"]
 
 
 def kernel_times():

@@ -1,0 +1,95 @@
+"""GPU: the device fairness regulariser, label-pattern weights and train
+metrics (csrc/fairness.hip through mpvae_fair.py) against the golden vectors
+recorded from the reference and against the oracle at training sizes."""
+import numpy as np
+import pytest
+import torch
+
+import mpvae_fair as mf
+from fair_io import fair_fixtures, metric_fixtures
+from oracle import fairness as of
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+FAIR = fair_fixtures()
+MET = metric_fixtures()
+
+
+def _run(f, dists=None, norm=None, coeff=None):
+    dists = f["dists"] if dists is None else dists
+    L = f["labels"].shape[1]
+    tables = [mf.LabelDistanceTable(d, L, DEV) for d in dists]
+    lz = torch.from_numpy(f["label_z"]).to(DEV).requires_grad_(True)
+    fz = torch.from_numpy(f["feat_z"]).to(DEV).requires_grad_(True)
+    loss, count = mf.fairness_penalty(lz, fz, torch.from_numpy(f["labels"]).to(DEV),
+                                      torch.from_numpy(f["sensitive"]).to(DEV), tables,
+                                      f["norm"] if norm is None else norm,
+                                      f["coeff"] if coeff is None else coeff)
+    loss.backward()
+    return loss, count, lz.grad, fz.grad
+
+
+@pytest.mark.parametrize("f", FAIR, ids=[f["name"] for f in FAIR])
+def test_fair_penalty_matches_reference(f):
+    loss, count, gl, gf = _run(f)
+    assert int(count) == int(f["contributed"])
+    if not int(f["active"]):
+        assert float(loss) == 0.0 and float(gl.abs().max()) == 0.0
+        return
+    ref = float(f["fairloss"])
+    assert loss.dtype == torch.float64
+    assert abs(float(loss) - ref) <= 1e-12 * abs(ref)
+    for g, r in ((gl, f["g_label_z"]), (gf, f["g_feat_z"])):
+        # fp64 on both sides, fp32 at the leaf: a few fp32 ulps
+        assert np.abs(g.cpu().numpy() - r).max() <= 1e-6 * np.abs(r).max()
+
+
+@pytest.mark.parametrize("norm", ["l1", "l2"])
+def test_fair_penalty_training_size_against_oracle(norm):
+    rng = np.random.default_rng(7)
+    B, L = 512, 1024
+    labels = (rng.random((B, L)) < 0.02).astype(np.int64)
+    labels[256:] = labels[:256]
+    sens = rng.integers(0, 3, (B, 2)).astype(np.int64)
+    dists = [{"".join(r.astype(str)): float(rng.uniform(0.1, 1)) for r in labels[i::7]}
+             for i in range(3)]
+    f = dict(labels=labels, sensitive=sens, dists=dists, norm=norm, coeff=0.5,
+             label_z=rng.uniform(0.01, 0.99, (B, L)).astype(np.float32),
+             feat_z=rng.uniform(0.01, 0.99, (B, L)).astype(np.float32))
+    loss, count, gl, gf = _run(f)
+    rl, rc, rgl, rgf = of.fair_penalty(f["label_z"], f["feat_z"], labels, sens, dists, norm, 0.5)
+    assert int(count) == rc
+    assert abs(float(loss) - rl) <= 1e-10 * abs(rl)
+    for g, r in ((gl, rgl), (gf, rgf)):
+        assert np.abs(g.cpu().numpy() - r).max() <= 1e-6 * np.abs(r).max()
+
+
+def test_label_weights_multiword_and_misses():
+    rng = np.random.default_rng(3)
+    B, L = 64, 200
+    labels = (rng.random((B, L)) < 0.1).astype(np.float32)
+    labels[5, 7] = 2.0                         # int() not 0/1: a miss, as in the reference
+    d = {"".join(r.astype(int).astype(str)): float(i + 1) for i, r in enumerate(labels[::2])}
+    tab = mf.LabelDistanceTable(d, L, DEV)
+    w, count = mf.label_weights(torch.from_numpy(labels).to(DEV), [tab])
+    ref = of.row_weights(labels, d)
+    assert np.array_equal(w.cpu().numpy()[0], ref)
+    assert int(count) == int((ref > 0).sum())
+
+
+@pytest.mark.parametrize("m", MET, ids=[m["name"] for m in MET])
+def test_train_metrics_match_reference(m):
+    res = mf.compute_metrics(torch.from_numpy(m["pred"]).to(DEV),
+                             torch.from_numpy(m["target"]).to(DEV), 0.5)
+    v = np.array([float(res[k]) for k in mf.METRIC_KEYS])
+    assert np.allclose(v, m["values"], rtol=1e-6, atol=1e-7), (v, m["values"])
+
+
+def test_train_metrics_training_size_against_oracle():
+    rng = np.random.default_rng(11)
+    B, L = 512, 1024
+    t = (rng.random((B, L)) < 0.05).astype(np.float32)
+    p = rng.random((B, L)).astype(np.float32)
+    res = mf.compute_metrics(torch.from_numpy(p).to(DEV), torch.from_numpy(t).to(DEV), 0.5)
+    v = np.array([float(res[k]) for k in mf.METRIC_KEYS])
+    assert np.allclose(v, of.train_metrics(p, t, 0.5), rtol=2e-6, atol=1e-7)
