@@ -186,12 +186,19 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   }
 }
 
-template <bool VEC, bool PLANES>
+// Rows of T in flight per thread beyond the one computing (MPV_ELEM_LA), and
+// ONE: a block row covers all its columns (RPI == 1), so the row index and the
+// six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
+#ifndef MPV_ELEM_LA
+#define MPV_ELEM_LA 3
+#endif
+template <bool VEC, bool PLANES, bool ONE>
 __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
+  constexpr int LA = MPV_ELEM_LA;
   __shared__ float cred[256 * 8];
   const int b = blockIdx.x, sc = blockIdx.y;
   const int tid = threadIdx.x;
-  const int rsub = tid / p.TPR, cq = tid % p.TPR;
+  const int rsub = ONE ? 0 : tid / p.TPR, cq = ONE ? tid : tid % p.TPR;
   const bool active = rsub < p.RPI;
   const int c0 = blockIdx.z * 1024 + cq * 4;
   const int S = p.S, B = p.B, L = p.L;
@@ -229,14 +236,16 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
   if (active && c0 < p.Lc) {
-    // two rows of lookahead: rows s+RPI and s+2RPI are in flight while row s
+    // LA rows of lookahead: rows s+RPI .. s+LA*RPI are in flight while row s
     // computes (the element math and the T stream overlap)
-    const int s0 = s_begin + rsub, R = p.RPI;
-    ElemRow cur, nx1, nx2;
-    if (s0 < s_end) elem_row_load<VEC>(cur, p, b, s0, c0, ok);
-    if (s0 + R < s_end) elem_row_load<VEC>(nx1, p, b, s0 + R, c0, ok);
+    const int s0 = s_begin + rsub, R = ONE ? 1 : p.RPI;
+    ElemRow buf[LA + 1];
+#pragma unroll
+    for (int j = 0; j < LA; ++j)
+      if (s0 + j * R < s_end) elem_row_load<VEC>(buf[j], p, b, s0 + j * R, c0, ok);
     for (int s = s0; s < s_end; s += R) {
-      if (s + 2 * R < s_end) elem_row_load<VEC>(nx2, p, b, s + 2 * R, c0, ok);
+      if (s + LA * R < s_end) elem_row_load<VEC>(buf[LA], p, b, s + LA * R, c0, ok);
+      const ElemRow& cur = buf[0];
       const int64_t cb = (int64_t)b * S + s;
       float G[4];
       f32x2 g2[4];
@@ -271,8 +280,8 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
             if (ok[q]) row[c0 + q] = G[q];
         }
       }
-      cur = nx1;
-      nx1 = nx2;
+#pragma unroll
+      for (int j = 0; j < LA; ++j) buf[j] = buf[j + 1];
     }
   }
   // column sums over this block's rows: reduce the RPI row-lanes per column
@@ -1224,11 +1233,14 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   const dim3 eg(B, pl.nSc, pl.nLc);
   const bool vec = (L & 3) == 0;
   if (want_planes) {
-    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true>), eg, dim3(256), 0, st, ep);
-    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, true>), eg, dim3(256), 0, st, ep);
+    if (vec && pl.RPI == 1)
+      MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, true>), eg, dim3(256), 0, st, ep);
+    else if (vec)
+      MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, false>), eg, dim3(256), 0, st, ep);
+    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, true, false>), eg, dim3(256), 0, st, ep);
   } else {
-    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false>), eg, dim3(256), 0, st, ep);
-    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, false>), eg, dim3(256), 0, st, ep);
+    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false, false>), eg, dim3(256), 0, st, ep);
+    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, false, false>), eg, dim3(256), 0, st, ep);
   }
   if (int rc = check_launch("bwd_elem")) return rc;
   if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))

@@ -25,7 +25,8 @@ case "$1" in
     for v in $VARIANTS; do
       d=$(dir_of "$v")
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined \
-        -o "$d/libmpvae_hip.so" "$d/probit_fwd.o" "$d/probit_bwd.o" build/util.o || exit 1
+        -o "$d/libmpvae_hip.so" "$d/probit_fwd.o" "$d/probit_bwd.o" \
+        $(ls build/*.o | grep -v "build/probit_") || exit 1
     done ;;
   run)
     mkdir -p "$R/gpurun_out/abl"
