@@ -345,6 +345,9 @@ __device__ unsigned long long g_dr_stamps[2][8][32][4];
   do {               \
   } while (0)
 #endif
+#ifndef MPV_DR_UNROLL2
+#define MPV_DR_UNROLL2 0
+#endif
 #ifndef MPV_DR_KIND
 #define MPV_DR_KIND 1  // 0: 16x16x32 ring, 1: 16x16x32 staggered, 2: 32x32x16 4-deep ring, 3: 2 staggered
 #endif
@@ -638,45 +641,75 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   barrier_raw();
   DrFrag<TM, TN> f;
   // the two groups run the same number of barriers: 2*nst + 1
+  // MPV_DR_UNROLL2 (study, off): two stages per iteration, so that each
+  // stage image's LDS base is a compile-time offset and the fragment reads
+  // need no per-read address arithmetic (78 VALU per 96 MFMAs today).  The
+  // hoisted addresses do not fit beside 128 accumulator + 96 fragment VGPRs:
+  // 84 VGPRs spill.
+#define DR_G0_STAGE(i, PAR)                                                                   \
+  do {                                                                                        \
+    const int ci = (i);                                                                       \
+    (void)ci;                                                                                 \
+    MPV_STAMP(0);                                                                             \
+    if ((i) + 1 < nst)                                                                        \
+      drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
+                                  rows, wn, l0, z0, lane_u, lane_h);                          \
+    MPV_STAMP(1);                                                                             \
+    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
+    lds_barrier();                                                                            \
+    MPV_STAMP(2);                                                                             \
+    __builtin_amdgcn_s_setprio(1);                                                            \
+    dr_mfma<TM, TN>(acc, f);                                                                  \
+    __builtin_amdgcn_s_setprio(0);                                                            \
+    wait_vmcnt<0>();                                                                          \
+    MPV_STAMP(3);                                                                             \
+    barrier_raw();                                                                            \
+  } while (0)
+#define DR_G1_STAGE(i, PAR)                                                      \
+  do {                                                                           \
+    const int ci = (i);                                                          \
+    (void)ci;                                                                    \
+    MPV_STAMP(0);                                                                \
+    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp); \
+    MPV_STAMP(1);                                                                \
+    lds_barrier();                                                               \
+    MPV_STAMP(2);                                                                \
+    __builtin_amdgcn_s_setprio(1);                                               \
+    dr_mfma<TM, TN>(acc, f);                                                     \
+    __builtin_amdgcn_s_setprio(0);                                               \
+    MPV_STAMP(3);                                                                \
+    barrier_raw();                                                               \
+  } while (0)
   if (grp == 0) {
-    for (int i = 0; i < nst; ++i) {
-      const int ci = i;
-      MPV_STAMP(0);
-      // slot 2i: stream stage i+1, read stage i
-      if (i + 1 < nst)
-        drs_issue<PER_WAVE, PIECES>(p, smem + ((i + 1) & 1) * STAGE, q_begin + (i + 1) * kDrKR,
-                                    rows, wn, l0, z0, lane_u, lane_h);
-      MPV_STAMP(1);
-      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
-      lds_barrier();
-      MPV_STAMP(2);
-      // slot 2i+1: MFMAs of stage i; stage i+1 landed before the barrier
-      __builtin_amdgcn_s_setprio(1);
-      dr_mfma<TM, TN>(acc, f);
-      __builtin_amdgcn_s_setprio(0);
-      wait_vmcnt<0>();
-      MPV_STAMP(3);
-      barrier_raw();
+    // slot 2i: stream stage i+1, read stage i; slot 2i+1: MFMAs of stage i
+    // (stage i+1 landed before its barrier)
+    if (MPV_DR_UNROLL2) {
+      int i = 0;
+      for (; i + 1 < nst; i += 2) {
+        DR_G0_STAGE(i, 0);
+        DR_G0_STAGE(i + 1, 1);
+      }
+      if (i < nst) DR_G0_STAGE(i, 0);
+    } else {
+      for (int i = 0; i < nst; ++i) DR_G0_STAGE(i, i & 1);
     }
     barrier_raw();
   } else {
     barrier_raw();
-    for (int i = 0; i < nst; ++i) {
-      const int ci = i;
-      MPV_STAMP(0);
-      // slot 2i+1: read stage i
-      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
-      MPV_STAMP(1);
-      lds_barrier();
-      MPV_STAMP(2);
-      // slot 2i+2: MFMAs of stage i
-      __builtin_amdgcn_s_setprio(1);
-      dr_mfma<TM, TN>(acc, f);
-      __builtin_amdgcn_s_setprio(0);
-      MPV_STAMP(3);
-      barrier_raw();
+    // slot 2i+1: read stage i; slot 2i+2: MFMAs of stage i
+    if (MPV_DR_UNROLL2) {
+      int i = 0;
+      for (; i + 1 < nst; i += 2) {
+        DR_G1_STAGE(i, 0);
+        DR_G1_STAGE(i + 1, 1);
+      }
+      if (i < nst) DR_G1_STAGE(i, 0);
+    } else {
+      for (int i = 0; i < nst; ++i) DR_G1_STAGE(i, i & 1);
     }
   }
+#undef DR_G0_STAGE
+#undef DR_G1_STAGE
   const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
 #pragma unroll
   for (int m = 0; m < TM; ++m)
