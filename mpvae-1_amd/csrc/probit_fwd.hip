@@ -80,6 +80,16 @@ struct FwdParams {
 #ifndef MPV_T_NT
 #define MPV_T_NT 0
 #endif
+// forward with the epilogue pipelined into the next tile's K loop
+// (probit_fwd16p_kernel; study, off): parity-correct, but 18.6 ms (1 VALU
+// filler per MFMA) / 20.2 ms (2) / 29.9 ms (no interleave) against 14.5 ms:
+// two accumulator sets + fragments spill 60 VGPRs
+#ifndef MPV_FWD_P
+#define MPV_FWD_P 0
+#endif
+#ifndef MPV_FWDP_FILL
+#define MPV_FWDP_FILL 2
+#endif
 #ifndef MPV_EPI_SB
 #define MPV_EPI_SB 4
 #endif
@@ -1106,6 +1116,333 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   }
 }
 
+// --------------------- 3xf16, epilogue pipelined into the next tile (fwd16p)
+// probit_fwd16t with the epilogue of tile i run INSIDE the K loop of tile
+// i+1, by the same waves: in probit_fwd16t every wave reaches the epilogue
+// together and the matrix pipe idles for about a third of each tile.  Each
+// wave keeps the previous tile's 64 accumulators (pacc) beside the current
+// ones; the K loop's first 32 stages each carry one "unit" of the previous
+// tile's epilogue -- one sample group n (16 samples, the lane's sample lr)
+// x 2 of the lane's 4 labels of label group mg -- and the scheduler is told
+// to interleave its VALU with the stage's 48 MFMAs (sched_group_barrier:
+// one MFMA, then up to two VALU).  Row statistics go out per sample group
+// into an LDS accumulator (ds_add), column sums per label group; one extra
+// barrier per tile publishes the row statistics.  The last tile's epilogue
+// runs after the loop without MFMAs.  Needs nK >= 32 (z > 992): 32 units per
+// tile; L % 4 == 0.  Same arithmetic as probit_fwd16t, other summation
+// order of the row sums (deterministic).
+namespace fwdp {
+constexpr int WL = 4, WS = 2, TL = 4, TS = 4, NW = 8, NSTAGE = 2;
+constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // 128 samples, 256 labels
+constexpr int STAGE = (BM + BN) * kRowB;             // 48 KB
+constexpr int RED = WL * BM * 6, CACC = WS * BN * 2, COLS = BN * 8;  // floats
+}  // namespace fwdp
+
+// Per-label constants of the label tile, 8 floats per label:
+// fe, fx, qa, qb, sg (ranking exponent in log2 units), wpos, wneg, y.
+MPV_DEV void fwdp_cols_stage(float* cols, const FwdParams& p, int b, int n0) {
+  for (int i = threadIdx.x; i < fwdp::BN; i += fwdp::NW * 64) {
+    const int l = n0 + i;
+    const bool ok = l < p.L;
+    const int64_t o = (int64_t)b * p.L + (ok ? l : 0);
+    const float y = ok ? p.y[o] : 0.0f;
+    const bool hard = ok && (y == 0.0f || y == 1.0f);
+    float* c = cols + i * 8;
+    c[0] = ok ? p.fe[o] : 0.0f;
+    c[1] = ok ? p.fx[o] : 0.0f;
+    c[2] = !hard ? 0.0f : (y == 0.0f ? -1.0f : 1.0f);  // q = qa E + qb
+    c[3] = !hard ? 1.0f : (y == 0.0f ? 1.0f : 0.0f);
+    c[4] = y == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
+    c[5] = (ok && y == 1.0f) ? 1.0f : 0.0f;
+    c[6] = (ok && y == 0.0f) ? 1.0f : 0.0f;
+    c[7] = ok ? y : 0.0f;
+  }
+}
+
+// Unit (n, h) of the previous tile for label group mg: labels lb+2h, lb+2h+1.
+template <int H, bool SOFT>
+MPV_DEV void fwdp_unit(const f32x4& t4, const float* cols, int lb, float wr, f32x2& sl,
+                       f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
+  const f32x4 ca = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H) * 8);
+  const f32x4 cb = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H) * 8 + 4);
+  const f32x4 da = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H + 1) * 8);
+  const f32x4 db = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H + 1) * 8 + 4);
+  const f32x2 u[2] = {splat2(t4[2 * H]) + f32x2{ca[0], ca[1]},
+                      splat2(t4[2 * H + 1]) + f32x2{da[0], da[1]}};
+  f32x2 E[2];
+  probit_prob2xN<2>(u, E);
+  const f32x2 q0 = pk_fma(E[0], splat2(ca[2]), splat2(ca[3]));
+  const f32x2 q1 = pk_fma(E[1], splat2(da[2]), splat2(da[3]));
+  const f32x2 a0 = E[0] * cb[0], a1 = E[1] * db[0];
+  const f32x2 r0 = f32x2{__builtin_amdgcn_exp2f(a0.x), __builtin_amdgcn_exp2f(a0.y)};
+  const f32x2 r1 = f32x2{__builtin_amdgcn_exp2f(a1.x), __builtin_amdgcn_exp2f(a1.y)};
+  const f32x2 q = q0 * q1;  // >= (4.7e-7)^2: one log for both labels
+  f32x2 lp = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)};
+  if (SOFT) {  // a soft label adds both BCE terms (its q is 1); branch-free
+    const float y0 = cb[3], y1 = db[3];
+    // weight 1 for a soft label (qa = 0, y != 0; pad labels have y = 0), else 0
+    const float w0 = (ca[2] == 0.0f && y0 != 0.0f) ? 1.0f : 0.0f;
+    const float w1 = (da[2] == 0.0f && y1 != 0.0f) ? 1.0f : 0.0f;
+    const f32x2 o0 = splat2(1.0f) - E[0], o1 = splat2(1.0f) - E[1];
+    lp += splat2(w0) * f32x2{y0 * __builtin_amdgcn_logf(E[0].x) + (1.0f - y0) * __builtin_amdgcn_logf(o0.x),
+                             y0 * __builtin_amdgcn_logf(E[0].y) + (1.0f - y0) * __builtin_amdgcn_logf(o0.y)};
+    lp += splat2(w1) * f32x2{y1 * __builtin_amdgcn_logf(E[1].x) + (1.0f - y1) * __builtin_amdgcn_logf(o1.x),
+                             y1 * __builtin_amdgcn_logf(E[1].y) + (1.0f - y1) * __builtin_amdgcn_logf(o1.y)};
+  }
+  sl = sl + lp;
+  sp = pk_fma(splat2(cb[1]), r0, pk_fma(splat2(db[1]), r1, sp));
+  sn = pk_fma(splat2(cb[2]), r0, pk_fma(splat2(db[2]), r1, sn));
+  ce[2 * H] = pk_fma(splat2(wr), E[0], ce[2 * H]);
+  ce[2 * H + 1] = pk_fma(splat2(wr), E[1], ce[2 * H + 1]);
+}
+
+// Stage reads + MFMAs of one K stage (fragments of R per label group just in
+// time), optionally with one epilogue unit interleaved.
+template <bool UNIT, int H, bool SOFT>
+MPV_DEV void fwdp_stage(f32x4 (&acc)[fwdp::TL][fwdp::TS], const char* base, int wl, int ws, int lr,
+                        int coh, int col, const f32x4& t4, const float* cols, int lb, float wr,
+                        f32x2& sl, f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
+  using namespace fwdp;
+  FragT<TL, TS> f;
+  fwd16t_read<WL, TL, TS, BM>(f, base, wl, ws, lr, coh, col);
+  if (UNIT) fwdp_unit<H, SOFT>(t4, cols, lb, wr, sl, sp, sn, ce);
+  fwd16t_mfma<TL, TS>(acc, f);
+  if (UNIT && MPV_FWDP_FILL > 0) {
+    // interleave: the unit's VALU between the stage's MFMAs
+#pragma unroll
+    for (int i = 0; i < 48; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, MPV_FWDP_FILL, 0);  // VALU fillers
+    }
+  }
+}
+
+// Row statistics of sample group n (both halves done): reduce over the 4 lane
+// rows and accumulate into red (this wave owns these entries: plain LDS adds).
+MPV_DEV void fwdp_rowstats(float* red, int wl, int ws, int n, int lr, int lg, f32x2& sl, f32x2& sp,
+                           f32x2& sn) {
+  using namespace fwdp;
+  sl = sl * 0.6931471805599453f;
+  const float v[6] = {sl.x, sl.y, sp.x, sn.x, sp.y, sn.y};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const float tot = sum_lanegroups(v[k]);
+    if (lg == 0) atomicAdd(red + (wl * BM + (ws * TS + n) * 16 + lr) * 6 + k, tot);
+  }
+  sl = sp = sn = splat2(0.0f);
+}
+
+// the kernel's LDS (file scope, so that both instantiations of fwdp_main
+// address it as LDS directly)
+__shared__ __attribute__((aligned(1024))) char fwdp_smem[fwdp::NSTAGE * fwdp::STAGE +
+                                                         (fwdp::RED + fwdp::CACC + fwdp::COLS) * 4];
+
+template <bool SOFT>
+MPV_DEV void fwdp_main(const FwdParams& p) {
+  using namespace fwdp;
+  char* smem = fwdp_smem;
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL, ws = wid / WL;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int S = p.S, L = p.L;
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;  // >= 32 (host check)
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+  constexpr int NWD = NW / 2;  // the prio-1 half issues the stage DMA
+  const bool dmaw = wid >= NW / 2;
+  Fwd16Dma<BM, BN, NWD> dma;
+  dma.init(p, t_begin, b, n0, wid - NW / 2, lane);
+  if (dmaw) {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+  if (dmaw) __builtin_amdgcn_s_setprio(1);
+
+  f32x4 acc[TL][TS], pacc[TL][TS];
+  int gs = 0;
+  int prev_s0 = 0, prev_own = 0;
+  f32x2 sl = splat2(0.f), sp = splat2(0.f), sn = splat2(0.f);
+  f32x2 ce[4];
+
+  // one K stage: wait for its DMA, barrier, stream the next stage
+#define stage_head()                                                                      \
+  do {                                                                                    \
+    wait_vmcnt<0>();                                                                      \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                    \
+    barrier_raw(); /* stage gs landed for every wave; every wave is done reading gs-1 */  \
+    if (dmaw) dma.issue(p, fwdp_smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) %   \
+                                        NSTAGE) * STAGE, t_end, nK, b);                       \
+  } while (0)
+  // after the 8 units of label group mg: column sums into cacc, rotate pacc
+  auto group_tail = [&](int mg) {
+    const int lb = (wl * TL + mg) * 16 + lg * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
+      if (lr == 15) {
+        float* c = cacc + (ws * BN + lb + i) * 2;
+        c[0] += e;
+        c[1] += x;
+      }
+      ce[i] = splat2(0.0f);
+    }
+#pragma unroll
+    for (int mm = 0; mm + 1 < TL; ++mm)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) pacc[mm][n] = pacc[mm + 1][n];
+  };
+  // the previous tile's row statistics: red -> rowpart (one extra barrier)
+  auto publish_rows = [&]() {
+    lds_barrier();
+    for (int r = tid; r < BM; r += NW * 64) {
+      const int s = prev_s0 + r;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < WL; ++w) {
+          v += red[(w * BM + r) * 6 + k];
+          red[(w * BM + r) * 6 + k] = 0.0f;
+        }
+        if (s >= prev_own && s < S) p.rowpart[(((int64_t)k * p.nNt + nt) * p.B + b) * S + s] = v;
+      }
+    }
+  };
+  // unit j (0..7) of label group mg of the previous tile: sample group n = j/2, half j%2
+#define FWDP_UNIT_ARGS(J)                                                                   \
+  pacc[0][(J) / 2], cols, (wl * TL + mg) * 16 + lg * 4,                                     \
+      (prev_s0 + (ws * TS + (J) / 2) * 16 + lr >= prev_own &&                                 \
+       prev_s0 + (ws * TS + (J) / 2) * 16 + lr < S) ? 1.0f : 0.0f,                            \
+      sl, sp, sn, ce
+  // T stash of sample group n of the previous tile (16 B per lane, 4 labels)
+  auto store_t = [&](int mg, const f32x4& t4, int n) {
+    const int s = prev_s0 + (ws * TS + n) * 16 + lr;
+    const int lb = (wl * TL + mg) * 16 + lg * 4;
+    if (s >= prev_own && s < S && n0 + lb < L)
+      *reinterpret_cast<f32x4*>(p.T + ((int64_t)b * S + s) * L + n0 + lb) = t4;
+  };
+
+  bool have_prev = false;
+  for (int st = t_begin; st <= t_end; ++st) {
+    const bool mf = st < t_end;  // uniform
+    const int s0 = mf ? fwd_tile_s0<BM>(st, S) : 0;
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ce[i] = splat2(0.0f);
+    if (mf && have_prev) {
+      for (int mg = 0; mg < TL; ++mg) {
+#define FWDP_STEP(J)                                                                          \
+  do {                                                                                        \
+    stage_head();                                                                             \
+    if ((J) % 2 == 0) store_t(mg, pacc[0][(J) / 2], (J) / 2);                                  \
+    fwdp_stage<true, (J) % 2, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col,         \
+                              FWDP_UNIT_ARGS(J));                                             \
+    if ((J) % 2 == 1) fwdp_rowstats(red, wl, ws, (J) / 2, lr, lg, sl, sp, sn);                  \
+    ++gs;                                                                                     \
+  } while (0)
+        FWDP_STEP(0); FWDP_STEP(1); FWDP_STEP(2); FWDP_STEP(3);
+        FWDP_STEP(4); FWDP_STEP(5); FWDP_STEP(6); FWDP_STEP(7);
+#undef FWDP_STEP
+        group_tail(mg);
+      }
+      for (int kc = 32; kc < nK; ++kc, ++gs) {
+        stage_head();
+        fwdp_stage<false, 0, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col, acc[0][0],
+                             cols, 0, 0.0f, sl, sp, sn, ce);
+      }
+      publish_rows();
+    } else if (mf) {  // first tile: nothing to overlap
+      for (int kc = 0; kc < nK; ++kc, ++gs) {
+        stage_head();
+        fwdp_stage<false, 0, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col, acc[0][0],
+                             cols, 0, 0.0f, sl, sp, sn, ce);
+      }
+    } else if (have_prev) {  // drain: the last tile's epilogue alone
+      for (int mg = 0; mg < TL; ++mg) {
+#define FWDP_DRAIN(J)                                                                         \
+  do {                                                                                        \
+    if ((J) % 2 == 0) store_t(mg, pacc[0][(J) / 2], (J) / 2);                                  \
+    fwdp_unit<(J) % 2, SOFT>(FWDP_UNIT_ARGS(J));                                                    \
+    if ((J) % 2 == 1) fwdp_rowstats(red, wl, ws, (J) / 2, lr, lg, sl, sp, sn);                  \
+  } while (0)
+        FWDP_DRAIN(0); FWDP_DRAIN(1); FWDP_DRAIN(2); FWDP_DRAIN(3);
+        FWDP_DRAIN(4); FWDP_DRAIN(5); FWDP_DRAIN(6); FWDP_DRAIN(7);
+#undef FWDP_DRAIN
+        group_tail(mg);
+      }
+      publish_rows();
+    }
+    if (mf) {
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TS; ++n) pacc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
+      prev_s0 = s0;
+      prev_own = st * BM;
+    }
+    have_prev = mf;
+  }
+#undef FWDP_UNIT_ARGS
+#undef stage_head
+  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
+  lds_barrier();
+  for (int c = tid; c < BN; c += NW * 64) {
+    const int l = n0 + c;
+    if (l < L) {
+      float e = 0.f, x = 0.f;
+#pragma unroll
+      for (int w = 0; w < WS; ++w) {
+        e += cacc[(w * BN + c) * 2 + 0];
+        x += cacc[(w * BN + c) * 2 + 1];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * L + l] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * L + l] = x;
+    }
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void probit_fwd16p_kernel(FwdParams p) {
+  using namespace fwdp;
+  char* smem = fwdp_smem;
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x;
+  fwdp_cols_stage(cols, p, b, n0);
+  for (int i = tid; i < CACC + RED; i += NW * 64) red[i] = 0.0f;  // red, cacc adjacent
+  bool my_soft = false;
+  for (int i = tid; i < BN; i += NW * 64) {
+    const int l = n0 + i;
+    if (l < p.L) {
+      const float yv = p.y[(int64_t)b * p.L + l];
+      my_soft |= !(yv == 0.0f || yv == 1.0f);
+    }
+  }
+  // readfirstlane: the compiler must see the branch (around the whole main
+  // loop) as uniform, or every value inside turns divergent
+  if (__builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)))  // two-log BCE terms
+    fwdp_main<true>(p);
+  else
+    fwdp_main<false>(p);
+}
+
 // One block per batch row b.  rowpart -> rowstat, bstat.
 __global__ __launch_bounds__(256) void fwd_combine_kernel(const float* __restrict__ y,
                                                          const float* __restrict__ rowpart,
@@ -1360,7 +1697,13 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   p.nSt = pl.nSt;
   const int64_t blocks = (int64_t)shape->B * pl.nSc * pl.nNt;
   MPV_REQUIRE(blocks < (int64_t(1) << 31), "grid too large");
-  launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
+  const bool pipelined = MPV_FWD_P && a->gemm == MPV_GEMM_F16X3 && pl.cfg == 3 &&
+                         pl.BM == fwdp::BM && pl.BN == fwdp::BN && cdiv(shape->z, kKC) >= 32 &&
+                         shape->L % 4 == 0 && a->T != nullptr;
+  if (pipelined)
+    MPV_LAUNCH("probit_fwd", probit_fwd16p_kernel, dim3((unsigned)blocks), dim3(512), 0, st, p);
+  else
+    launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
   MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(256), 0, st, a->y,
              p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
