@@ -11,7 +11,8 @@ import mpvae_hip as H
 from mpvae_ops import ElboConfig, HipShardBackend, ProbitELBO
 from golden_io import DIFF, OUTS, PART_KEYS, fixtures
 from oracle import philox, probit_elbo as pe
-from tolerances import EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL, rel_err
+from tolerances import (EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL,
+                        LONG_K_GRAD_RTOL, rel_err)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -131,8 +132,9 @@ RANDOM_CASES = [
     (200, 64, 5, 257, 8),        # two column tiles, ragged s tiles
     (1024, 1024, 2, 48, 50),     # C4 dims, tiny batch
     (1030, 96, 2, 20, 8),        # L > 1024: two bwd column chunks
-    (1024, 1000, 2, 300, 8),     # pipelined forward epilogue: 3 sample tiles, ragged K
-    (260, 1024, 3, 257, 8),      # pipelined, pad labels in the last label tile
+    (1024, 1000, 2, 300, 8),     # 256-label tiles: 3 sample tiles, ragged K
+    (260, 1024, 3, 257, 8),      # 256-label tiles, pad labels in the last label tile
+    (4096, 4096, 1, 40, 8),      # C5 dims (16 label tiles, 128 K stages), S < one tile
 ]
 
 
@@ -166,9 +168,10 @@ def test_random_against_oracle(L, z, B, S, d, gemm):
     obj = out[0] + (out[6] * torch.from_numpy(g_I).to(DEV)).sum() + \
         (out[7] * torch.from_numpy(g_IL).to(DEV)).sum()
     obj.backward()
+    gtol = LONG_K_GRAD_RTOL if z >= 2048 else GRAD_RTOL
     for k in DIFF + ["r_sqrt_sigma"]:
         e = rel_err(_np(t[k].grad), rg[k])
-        assert e <= GRAD_RTOL, (k, e)
+        assert e <= gtol, (k, e)
 
 
 def test_shard_invariance_at_c4_size():

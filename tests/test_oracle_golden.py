@@ -100,3 +100,38 @@ def test_torch_restatement_matches_reference(f):
     obj.backward()
     for k in DIFF:
         assert rel_err(t[k].grad.numpy(), f["gtot_" + k]) <= 1e-5, k
+
+
+def test_long_k_gradient_conditioning():
+    """Rationale of LONG_K_GRAD_RTOL: at z = 4096 an fp32 noise GEMM (the
+    reference's own precision) alone moves the oracle's gradients by ~1e-4."""
+    from oracle import probit_elbo as pe
+    from tolerances import LONG_K_GRAD_RTOL, rel_err
+    L, z, B, S, d = 4096, 4096, 1, 40, 8
+    rng = np.random.default_rng(L * 7 + S)   # the GPU test's case
+    y = (rng.random((B, L)) < 0.25).astype(np.float32)
+    y[:, 0], y[:, 1] = 1, 0
+    f32 = lambda a: a.astype(np.float32)
+    # the GPU test's draw order (dict literal: fe_out, fx_out, fe_mu, fe_logvar, fx_mu, fx_logvar)
+    fe_out, fx_out = f32(rng.standard_normal((B, L))), f32(rng.standard_normal((B, L)))
+    fe_mu, fe_logvar = f32(rng.standard_normal((B, d))), f32(0.3 * rng.standard_normal((B, d)))
+    fx_mu, fx_logvar = f32(rng.standard_normal((B, d))), f32(0.3 * rng.standard_normal((B, d)))
+    inp = [y, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar]
+    R = rng.uniform(-1, 1, (L, z)) * np.sqrt(6.0 / (L + z))
+    noise = f32(rng.standard_normal((S, B, z)))
+    g_I, g_IL = f32(rng.standard_normal((B, L))), f32(rng.standard_normal((B, L)))
+
+    def grads():
+        ref = pe.elbo_forward(*inp, R, noise, 0.5, 10.0)
+        return pe.elbo_backward(ref, *inp, noise, 0.5, 10.0, g_total=1.0, g_I=g_I, g_IL=g_IL)
+
+    a = grads()
+    orig = pe.noise_product
+    try:
+        pe.noise_product = lambda n, r: (np.asarray(n, np.float32)
+                                         @ np.asarray(r).astype(np.float32).T).astype(np.float32)
+        b = grads()
+    finally:
+        pe.noise_product = orig
+    spread = max(rel_err(b[k], a[k]) for k in ("fe_out", "fx_out", "r_sqrt_sigma"))
+    assert 5e-5 < spread < LONG_K_GRAD_RTOL / 2, spread

@@ -17,6 +17,13 @@ checked at the looser level.
 
 FWD_RTOL = 2e-5
 GRAD_RTOL = 5e-5
+# Long noise GEMMs (z = 4096): the gradient w.r.t. fe_out / fx_out / R is
+# conditioned at the 1e-4 level by the fp32 rounding of t = eps . R^T alone:
+# the oracle with t from an fp32 sgemm (as the reference's own fp32
+# tensordot) instead of fp64 accumulation moves d fx_out by 1.05e-4 and dR by
+# 6.1e-5 on the test_random_against_oracle case (4096, 4096, 1, 40) --
+# measured, DESIGN.md section 4.  Allowed: 5x that spread.
+LONG_K_GRAD_RTOL = 5e-4
 EXTREME_FWD_RTOL = 1e-3
 EXTREME_GRAD_RTOL = 5e-2
 
