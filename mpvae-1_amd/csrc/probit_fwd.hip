@@ -562,19 +562,25 @@ struct Fwd16Dma {
     lds_dma16(base, off, lds_addr(dst));
   }
 
-  // Stream the next stage (if any) into stage image `dst`.
+  // Stream the next stage (if any) into stage image `dst` (PART 1: only the
+  // eps image, 2: only the R image, 0: both; the cursor advances either way).
+  template <int PART = 0>
   MPV_DEV void issue(const FwdParams& p, char* dst, int tile_end, int nK, int b) {
     if (tile >= tile_end) return;
     const int kb = kc * kRowB;  // byte offset of the K slice within a row
+    if (PART != 2) {
 #pragma unroll
-    for (int j = 0; j < JA; ++j) {
-      const int pc = wid + j * NW;
-      if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[j], dst + pc * 1024);
+      for (int j = 0; j < JA; ++j) {
+        const int pc = wid + j * NW;
+        if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[j], dst + pc * 1024);
+      }
     }
+    if (PART != 1) {
 #pragma unroll
-    for (int j = 0; j < JB; ++j) {
-      const int pc = wid + j * NW;
-      if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
+      for (int j = 0; j < JB; ++j) {
+        const int pc = wid + j * NW;
+        if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
+      }
     }
     ++issued;
     if (++kc == nK) {
@@ -1033,13 +1039,22 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
     }
   }
   const bool soft_any = __syncthreads_or(my_soft);
-  constexpr int NWD = MPV_FWD_DMAW ? NW / 2 : NW;  // DMA-issuing waves
-  const bool dmaw = MPV_FWD_DMAW == 0 || ((MPV_FWD_DMAW == 1) == (wid >= NW / 2));
+  // DMA split (MPV_FWD_DMAW): 0 all waves, 1 the prio-1 half, 2 the other
+  // half; 3/4: the R image by waves NW/2.. before their MFMAs and the eps
+  // image by waves 0..NW/2-1 after (3) or before (4) theirs
+  constexpr bool SPLIT = MPV_FWD_DMAW >= 3;
+  constexpr int NWD = MPV_FWD_DMAW ? NW / 2 : NW;  // DMA-issuing waves (per image if SPLIT)
+  const bool dmaw = SPLIT || MPV_FWD_DMAW == 0 || ((MPV_FWD_DMAW == 1) == (wid >= NW / 2));
+  const bool rwave = wid >= NW / 2;  // SPLIT: streams the R image
   Fwd16Dma<BM, BN, NWD> dma;
-  dma.init(p, t_begin, b, n0, MPV_FWD_DMAW == 1 ? wid - NW / 2 : wid % NWD, lane);
+  dma.init(p, t_begin, b, n0, (MPV_FWD_DMAW == 1 || SPLIT) ? wid % (NW / 2) : wid % NWD, lane);
   if (dmaw) {
 #pragma unroll
-    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+    for (int j = 0; j < NSTAGE - 1; ++j) {
+      if (!SPLIT) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+      else if (rwave) dma.template issue<2>(p, smem + j * STAGE, t_end, nK, b);
+      else dma.template issue<1>(p, smem + j * STAGE, t_end, nK, b);
+    }
   }
 
   int gs = 0;
@@ -1072,10 +1087,18 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
             acc, f, dma, dmaon, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
         if (dmaon) dma.advance(p, t_end, nK, b);
       } else {
-        if (dmaw) dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+        char* nxt = smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE;
+        if (!SPLIT) {
+          if (dmaw) dma.issue(p, nxt, t_end, nK, b);
+        } else if (rwave) {
+          dma.template issue<2>(p, nxt, t_end, nK, b);
+        } else if (MPV_FWD_DMAW == 4) {
+          dma.template issue<1>(p, nxt, t_end, nK, b);
+        }
         FWD_STAMP(3);
         fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
         fwd16t_mfma<TL, TS>(acc, f);
+        if (SPLIT && MPV_FWD_DMAW == 3 && !rwave) dma.template issue<1>(p, nxt, t_end, nK, b);
       }
     }
     FWD_ESTAMP(0);
