@@ -90,6 +90,9 @@ struct FwdParams {
 #ifndef MPV_FWDP_FILL
 #define MPV_FWDP_FILL 2
 #endif
+#ifndef MPV_COMBINE_T
+#define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
+#endif
 #ifndef MPV_EPI_SB
 #define MPV_EPI_SB 4
 #endif
@@ -1467,7 +1470,7 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16p_kernel(FwdParams p) {
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
-__global__ __launch_bounds__(256) void fwd_combine_kernel(const float* __restrict__ y,
+__global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restrict__ y,
                                                          const float* __restrict__ rowpart,
                                                          float* __restrict__ rowstat,
                                                          float* __restrict__ bstat, int S, int B,
@@ -1728,7 +1731,7 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   else
     launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
-  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(256), 0, st, a->y,
+  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(MPV_COMBINE_T), 0, st, a->y,
              p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
   if (int rc = check_launch("fwd_combine")) return rc;
   if (pl.nSc > 1) {

@@ -129,6 +129,9 @@ __global__ void sum_slabs_kernel(const float* __restrict__ in, int64_t nslab, in
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     float acc = 0.0f;
+    // fixed summation order (deterministic); unrolled so that the loads of
+    // several slabs are in flight together
+#pragma unroll 8
     for (int64_t k = 0; k < nslab; ++k) acc += in[k * n + i];
     out[i] = (D)acc;
   }
