@@ -38,7 +38,7 @@ int launch_scale(const float* block_max, int n, float* scale, hipStream_t s);
 constexpr float kBoundDl = 4.5f, kBoundPos = 0.4f, kBoundNeg = 60.0f, kBoundInd = 0.4f;
 
 // --------------------------------------------------------------- coefficients
-__global__ __launch_bounds__(256) void bwd_coef_kernel(
+__global__ __launch_bounds__(1024) void bwd_coef_kernel(
     const float* __restrict__ y, const float* __restrict__ rowstat, const float* __restrict__ bstat,
     const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
     float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
@@ -1229,7 +1229,7 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   const int S = (int)shape->S_local, B = (int)shape->B, L = (int)shape->L, z = (int)shape->z;
   const bool want_planes = planes && a->dR32 != nullptr;
 
-  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B), dim3(256), 0, st, a->y, a->rowstat, a->bstat,
+  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B), dim3(1024), 0, st, a->y, a->rowstat, a->bstat,
              a->gscal, a->g_indiv, a->g_indiv_label, coef, want_planes ? gbound : nullptr, S, B, L,
              (float)shape->S_total, a->nll_coeff, a->c_coeff, a->live);
   if (int rc = check_launch("bwd_coef")) return rc;

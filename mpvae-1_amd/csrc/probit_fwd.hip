@@ -1527,7 +1527,7 @@ __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restri
 }
 
 // Block 0: the six scalars; blocks >= 1: indiv_prob / indiv_prob_label.
-__global__ __launch_bounds__(256) void finalize_kernel(mpv_final_args a, int B, int L,
+__global__ __launch_bounds__(1024) void finalize_kernel(mpv_final_args a, int B, int L,
                                                       float S_total) {
   if (blockIdx.x > 0) {
     const int64_t n = (int64_t)B * L;
@@ -1550,6 +1550,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(mpv_final_args a, int B, 
   }
   float kl = 0.f;
   const int64_t nd = (int64_t)B * a.d;
+#pragma unroll 4
   for (int64_t i = tid; i < nd; i += blockDim.x) {
     const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
     const float dm = a.fx_mu[i] - a.fe_mu[i];
@@ -1748,9 +1749,9 @@ int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* a, void* s
                   a->indiv_prob && a->indiv_prob_label && a->d > 0,
               "NULL pointer in mpv_final_args");
   const int64_t n = shape->B * shape->L;
-  int64_t nb = cdiv(n, 256);
-  if (nb > 4096) nb = 4096;
-  MPV_LAUNCH("finalize", finalize_kernel, dim3((unsigned)(1 + nb)), dim3(256), 0,
+  int64_t nb = cdiv(n, 1024);
+  if (nb > 2048) nb = 2048;
+  MPV_LAUNCH("finalize", finalize_kernel, dim3((unsigned)(1 + nb)), dim3(1024), 0,
              as_stream(stream), *a, (int)shape->B, (int)shape->L, (float)shape->S_total);
   return check_launch("finalize");
 }
