@@ -549,8 +549,32 @@ MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0
   }
 }
 
+#ifndef MPV_MFMA_PHASED
+#define MPV_MFMA_PHASED 0
+#endif
 template <int TM, int TN>
 MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
+  if (MPV_MFMA_PHASED) {  // term by term over all tiles, same order per accumulator
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                           acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
+                                                           acc[m][n], 0, 0, 0);
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -574,7 +598,7 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
     const int pc = wn * PER_WAVE + i;  // wave-uniform
     const bool is_g = pc < PIECES / 2;
     const int r = is_g ? pc : pc - PIECES / 2;
-    const int q = q0 + r;
+    const int q = (MPV_ABL & 2048) ? ((q0 & 63) + r) : q0 + r;  // 2048: L2-resident rows (timing study)
     const char* src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
                            : reinterpret_cast<const char*>(p.eps16.data +
                                                            (int64_t)min(q, rows - 1) * p.eps16.ld +

@@ -93,6 +93,9 @@ struct FwdParams {
 #ifndef MPV_COMBINE_T
 #define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
 #endif
+#ifndef MPV_MFMA_PHASED
+#define MPV_MFMA_PHASED 1  // term-by-term MFMA issue (same per-accumulator order): -0.75 %
+#endif
 #ifndef MPV_EPI_SB
 #define MPV_EPI_SB 4
 #endif
@@ -803,6 +806,30 @@ MPV_DEV void fwd16t_mfma_dma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f, Dma& 
 
 template <int TL, int TS>
 MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
+  if (MPV_MFMA_PHASED) {
+    // the same products per accumulator in the same order (hi.hi, hi.lo,
+    // lo.hi), issued term by term over all tiles: consecutive MFMAs see
+    // operands of one kind (study: operand-toggle power)
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
+                                                           acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
+                                                           acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
+                                                           acc[m][n], 0, 0, 0);
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < TL; ++m)
 #pragma unroll
