@@ -93,6 +93,9 @@ struct FwdParams {
 #ifndef MPV_COMBINE_T
 #define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
 #endif
+#ifndef MPV_T_SPLIT
+#define MPV_T_SPLIT 1  // T stash per label group inside the epilogue label loop: -1.5 %
+#endif
 #ifndef MPV_MFMA_PHASED
 #define MPV_MFMA_PHASED 1  // term-by-term MFMA issue (same per-accumulator order): -0.75 %
 #endif
@@ -866,7 +869,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // T stash first, all label groups of a sample back to back: the 4 lane rows
   // x TL groups cover whole 128-B lines of the sample's T row (written while
   // still combinable in L2, rather than as half lines far apart in time)
-  if (!(MPV_ABL & 2) && p.T != nullptr) {
+  if (!(MPV_ABL & 2) && !MPV_T_SPLIT && p.T != nullptr) {
     const bool vecT = (L & 3) == 0;
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
@@ -904,6 +907,23 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + 1][n];
     const int lb = (wl * TL + m) * 16 + lg * 4;  // first of the lane's 4 labels in the tile
+    if (MPV_T_SPLIT && !(MPV_ABL & 2) && p.T != nullptr) {
+      // T stash of this label group (study: spread over the label loop)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) {
+        const int s = s0 + (ws * TS + n) * 16 + lr;
+        if (s >= s_own && s < S) {
+          float* row = p.T + ((int64_t)b * S + s) * L + n0;
+          if ((L & 3) == 0 && n0 + lb + 3 < L) {
+            *reinterpret_cast<f32x4*>(row + lb) = am[n];
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (n0 + lb + i < L) row[lb + i] = am[n][i];
+          }
+        }
+      }
+    }
     const f32x4 pa = *reinterpret_cast<const f32x4*>(cols + 2 * lb);  // (fe, fx) of labels 0, 1
     const f32x4 pb = *reinterpret_cast<const f32x4*>(cols + 2 * lb + 4);  // labels 2, 3
     const f32x2 fex[4] = {f32x2{pa[0], pa[1]}, f32x2{pa[2], pa[3]}, f32x2{pb[0], pb[1]},
