@@ -93,6 +93,9 @@ struct FwdParams {
 #ifndef MPV_COMBINE_T
 #define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
 #endif
+#ifndef MPV_FWD_NSTAGE
+#define MPV_FWD_NSTAGE 2  // stage ring depth of the 256 x 128 forward tile
+#endif
 #ifndef MPV_EPI_ALT
 #define MPV_EPI_ALT 1  // alternate the two SIMD partners priority per label group: -0.9 %
 #endif
@@ -857,7 +860,8 @@ MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
 template <int WL, int WS, int TL, int TS>
 MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
                                  int b, int s0, int s_own, int nt, float* red, float* cacc,
-                                 const float* cols, bool soft_any, int eidx) {
+                                 const float* cols, bool soft_any, int eidx,
+                                 bool sync_before_red = false) {
   constexpr int NT = WL * WS * 64, BM = WS * TS * 16, BN = WL * TL * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wl = wid % WL, ws = wid / WL, lr = lane & 15, lg = lane >> 4;
@@ -1025,6 +1029,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
   }
   FWD_ESTAMP2(2);
+  // red in a ring image: every wave must be past its last fragment read of it
+  if (sync_before_red) lds_barrier();
   // row statistics: sum over the 4 lane rows; lanes of row 0 publish
 #pragma unroll
   for (int n = 0; n < TS; ++n) {
@@ -1060,9 +1066,15 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
   constexpr int STAGE = (BM + BN) * kRowB;
   constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN) * 4];
-  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cacc = red + RED;
+  // With a 3-deep ring the epilogue's row-sum area lives in the ring image
+  // read last (free until the next K stage refills it): the 3 stage images
+  // + column sums + label constants then fit in 160 KB.
+  constexpr bool RED_IN_RING = NSTAGE >= 3;
+  static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
+  constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + 3 * BN) * 4];
+  float* red_own = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red_own + RED_OWN;
   float* cols = cacc + CACC;
 
   int g, nt;
@@ -1173,8 +1185,12 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
       p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
     } else {
       if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
+      // ring image read by the last K stage: stages gs, gs+1 are in flight
+      float* red = RED_IN_RING
+                       ? reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE)
+                       : red_own;
       fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                          soft_any, st - t_begin);
+                                          soft_any, st - t_begin, RED_IN_RING);
       if (MPV_EPI_PRIO >= 0) {  // back to the K-loop priorities
         if (MPV_FWD_PRIO && wid >= NW / 2)
           __builtin_amdgcn_s_setprio(MPV_FWD_PRIO);
@@ -1685,7 +1701,8 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         if (MPV_FWD_BIG)  // 256 labels x 256 samples, 8 waves of 128 x 64
           MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
         else
-          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, 2>), grid, dim3(512), 0, st, p);
+          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, MPV_FWD_NSTAGE>), grid,
+                     dim3(512), 0, st, p);
         break;
       default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
         if (MPV_FWD_T) {
