@@ -93,6 +93,11 @@ struct FwdParams {
 #ifndef MPV_COMBINE_T
 #define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
 #endif
+// asymmetric sample split of the 256 x 128 tile (probit_fwd16a): 16-sample
+// blocks of waves 0-3 (the waves 4-7 stream the DMA and own the rest); 4 = even
+#ifndef MPV_FWD_TSA
+#define MPV_FWD_TSA 5
+#endif
 #ifndef MPV_FWD_NSTAGE
 #define MPV_FWD_NSTAGE 2  // stage ring depth of the 256 x 128 forward tile
 #endif
@@ -771,7 +776,7 @@ struct FragT {
 };
 
 template <int WL, int TL, int TS, int BM>
-MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int ws, int lr, int coh,
+MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int sbo, int lr, int coh,
                          int col) {
 #pragma unroll
   for (int m = 0; m < TL; ++m) {
@@ -781,7 +786,7 @@ MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int ws, int
   }
 #pragma unroll
   for (int n = 0; n < TS; ++n) {
-    const int off = ((ws * TS + n) * 16 + lr) * kRowB;
+    const int off = ((sbo + n) * 16 + lr) * kRowB;
     f.eh[n] = *reinterpret_cast<const s16x8*>(base + off + coh);
     f.el[n] = *reinterpret_cast<const s16x8*>(base + off + col);
   }
@@ -857,14 +862,15 @@ MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
 // 16 per-label masks of a label group would otherwise pin ~40 SGPRs and spill.
 // Every element is finite (R pad rows are zero, eps rows are clamped), so
 // weighting instead of selecting is exact.
-template <int WL, int WS, int TL, int TS>
+template <int WL, int WS, int TL, int TS, int BMT = WS * TS * 16>
 MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
                                  int b, int s0, int s_own, int nt, float* red, float* cacc,
                                  const float* cols, bool soft_any, int eidx,
-                                 bool sync_before_red = false) {
-  constexpr int NT = WL * WS * 64, BM = WS * TS * 16, BN = WL * TL * 16;
+                                 bool sync_before_red = false, int sbo = -1) {
+  constexpr int NT = WL * WS * 64, BM = BMT, BN = WL * TL * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wl = wid % WL, ws = wid / WL, lr = lane & 15, lg = lane >> 4;
+  if (sbo < 0) sbo = ws * TS;  // first 16-sample block of this wave
   const int S = p.S, B = p.B, L = p.L, n0 = nt * BN;
   f32x2 sl[TS], sp[TS], sn[TS];  // per sample: log-prob, P, N (label .x / feature .y branch)
 #pragma unroll
@@ -880,7 +886,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const bool vecT = (L & 3) == 0;
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
-      const int s = s0 + (ws * TS + n) * 16 + lr;
+      const int s = s0 + (sbo + n) * 16 + lr;
       if (s >= s_own && s < S) {
         float* row = p.T + ((int64_t)b * S + s) * L + n0;
 #pragma unroll
@@ -927,7 +933,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       // T stash of this label group (study: spread over the label loop)
 #pragma unroll
       for (int n = 0; n < TS; ++n) {
-        const int s = s0 + (ws * TS + n) * 16 + lr;
+        const int s = s0 + (sbo + n) * 16 + lr;
         if (s >= s_own && s < S) {
           float* row = p.T + ((int64_t)b * S + s) * L + n0;
           if ((L & 3) == 0 && n0 + lb + 3 < L) {
@@ -963,7 +969,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
-      const int s = s0 + (ws * TS + n) * 16 + lr;
+      const int s = s0 + (sbo + n) * 16 + lr;
       const float wr = (s >= s_own && s < S) ? 1.0f : 0.0f;
       const f32x4 t4 = am[n];
       f32x2 uu[4], E4[4];
@@ -1039,7 +1045,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const float tot = sum_lanegroups(v[k]);
-      if (lg == 0) red[(wl * BM + (ws * TS + n) * 16 + lr) * 6 + k] = tot;
+      if (lg == 0) red[(wl * BM + (sbo + n) * 16 + lr) * 6 + k] = tot;
     }
   }
   FWD_ESTAMP2(3);
@@ -1155,7 +1161,7 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
       FWD_STAMP(2);
       FragT<TL, TS> f;
       if (MPV_FWD_SPREAD) {
-        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
+        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
         const bool dmaon = dma.active(t_end);
         fwd16t_mfma_dma<TL, TS, Fwd16Dma<BM, BN, NWD>::JA + Fwd16Dma<BM, BN, NWD>::JB>(
             acc, f, dma, dmaon, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
@@ -1170,7 +1176,7 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
           dma.template issue<1>(p, nxt, t_end, nK, b);
         }
         FWD_STAMP(3);
-        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col);
+        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
         fwd16t_mfma<TL, TS>(acc, f);
         if (SPLIT && MPV_FWD_DMAW == 3 && !rwave) dma.template issue<1>(p, nxt, t_end, nK, b);
       }
@@ -1200,6 +1206,121 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
     }
     FWD_ESTAMP(5);
   }
+  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
+  lds_barrier();
+  for (int c = tid; c < BN; c += NW * 64) {
+    const int l = n0 + c;
+    if (l < p.L) {
+      float e = 0.f, x = 0.f;
+#pragma unroll
+      for (int w = 0; w < WS; ++w) {
+        e += cacc[(w * BN + c) * 2 + 0];
+        x += cacc[(w * BN + c) * 2 + 1];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + l] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + l] = x;
+    }
+  }
+}
+
+// ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
+// probit_fwd16t's 256 x 128 tile with the 128 samples split unevenly between
+// the two waves of each SIMD: waves 0-3 own TSA 16-sample blocks, waves 4-7
+// TSB (< TSA) and stream every stage's DMA.  In probit_fwd16t both halves own
+// 64 samples; the DMA half then runs its 48 MFMAs after ~800 cycles of DMA
+// issue while the other half is already done and waits at the barrier.  Here
+// the DMA half has less MFMA work, so its DMA issue hides under the other
+// half's longer MFMA phase.
+template <int TSW>
+MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cacc,
+                          const float* cols, Fwd16Dma<128, 256, 4>& dma, bool dmaw, int b, int nt,
+                          int t_begin, int t_end, int nK, bool soft_any, int wl, int sbo, int lr,
+                          int coh, int col, float scale, bool prio1) {
+  constexpr int WL = 4, WS = 2, TL = 4, BM = 128, NSTAGE = 2;
+  constexpr int STAGE = (BM + 256) * kRowB;
+  int gs = 0;
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TSW];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TSW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      if (dmaw)
+        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
+                  t_end, nK, b);
+      FragT<TL, TSW> f;
+      fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+      fwd16t_mfma<TL, TSW>(acc, f);
+    }
+    if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
+    fwd_tile_epilogue_t<WL, WS, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                             soft_any, st - t_begin, false, sbo);
+    if (MPV_EPI_PRIO >= 0) {
+      if (prio1)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
+  }
+}
+
+template <int TSA, int TSB>
+__global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
+  constexpr int WL = 4, WS = 2, NW = 8, NSTAGE = 2;
+  constexpr int BM = (TSA + TSB) * 16, BN = 256;
+  static_assert(BM == 128, "the sample tile stays 128");
+  constexpr int STAGE = (BM + BN) * kRowB;
+  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN) * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL;
+  const int lr = lane & 15, lg = lane >> 4;
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  bool my_soft = false;
+  for (int i = tid; i < BN; i += NW * 64) {
+    const int l = n0 + i;
+    if (l < p.L) {
+      const float yv = p.y[(int64_t)b * p.L + l];
+      my_soft |= !(yv == 0.0f || yv == 1.0f);
+    }
+  }
+  const bool soft_any = __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
+  const bool dmaw = wid >= NW / 2;  // the TSB half streams the stages
+  Fwd16Dma<BM, BN, NW / 2> dma;
+  dma.init(p, t_begin, b, n0, wid % (NW / 2), lane);
+  if (dmaw) {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+  const bool prio1 = MPV_FWD_PRIO && dmaw;
+  if (prio1) __builtin_amdgcn_s_setprio(1);
+  if (wid < NW / 2)
+    fwd16a_tiles<TSA>(p, smem, red, cacc, cols, dma, false, b, nt, t_begin, t_end, nK, soft_any,
+                      wl, 0, lr, coh, col, scale, prio1);
+  else
+    fwd16a_tiles<TSB>(p, smem, red, cacc, cols, dma, true, b, nt, t_begin, t_end, nK, soft_any,
+                      wl, TSA, lr, coh, col, scale, prio1);
   // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
   lds_barrier();
   for (int c = tid; c < BN; c += NW * 64) {
@@ -1305,7 +1426,7 @@ MPV_DEV void fwdp_stage(f32x4 (&acc)[fwdp::TL][fwdp::TS], const char* base, int 
                         f32x2& sl, f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
   using namespace fwdp;
   FragT<TL, TS> f;
-  fwd16t_read<WL, TL, TS, BM>(f, base, wl, ws, lr, coh, col);
+  fwd16t_read<WL, TL, TS, BM>(f, base, wl, ws * TS, lr, coh, col);
   if (UNIT) fwdp_unit<H, SOFT>(t4, cols, lb, wr, sl, sp, sn, ce);
   fwd16t_mfma<TL, TS>(acc, f);
   if (UNIT && MPV_FWDP_FILL > 0) {
@@ -1701,8 +1822,12 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         if (MPV_FWD_BIG)  // 256 labels x 256 samples, 8 waves of 128 x 64
           MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
         else
-          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, MPV_FWD_NSTAGE>), grid,
-                     dim3(512), 0, st, p);
+          if (MPV_FWD_TSA != 4)
+            MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<MPV_FWD_TSA, 8 - MPV_FWD_TSA>), grid,
+                       dim3(512), 0, st, p);
+          else
+            MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, MPV_FWD_NSTAGE>), grid,
+                       dim3(512), 0, st, p);
         break;
       default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
         if (MPV_FWD_T) {
