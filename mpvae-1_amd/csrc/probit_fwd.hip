@@ -98,6 +98,9 @@ struct FwdParams {
 #ifndef MPV_FWD_TSA
 #define MPV_FWD_TSA 5
 #endif
+#ifndef MPV_FWD_XFER
+#define MPV_FWD_XFER 0  // rebalance the asymmetric forward's epilogue through LDS (study: +1 %)
+#endif
 #ifndef MPV_FWD_NSTAGE
 #define MPV_FWD_NSTAGE 2  // stage ring depth of the 256 x 128 forward tile
 #endif
@@ -1231,13 +1234,21 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
 // issue while the other half is already done and waits at the barrier.  Here
 // the DMA half has less MFMA work, so its DMA issue hides under the other
 // half's longer MFMA phase.
-template <int TSW>
+// IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).  With
+// MPV_FWD_XFER the epilogue is rebalanced: A hands its last X = (TSA-TSB)/2
+// blocks to B through LDS, and each wave decodes (TSA+TSB)/2 blocks (a wave
+// alone on its SIMD issues VALU at half the SIMD's rate, so the epilogue of
+// an uneven pair lasts as long as the bigger share).
+template <int TSW, bool IS_A, int TSA, int TSB>
 MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cacc,
-                          const float* cols, Fwd16Dma<128, 256, 4>& dma, bool dmaw, int b, int nt,
-                          int t_begin, int t_end, int nK, bool soft_any, int wl, int sbo, int lr,
-                          int coh, int col, float scale, bool prio1) {
+                          const float* cols, f32x4* xfer, Fwd16Dma<128, 256, 4>& dma, bool dmaw,
+                          int b, int nt, int t_begin, int t_end, int nK, bool soft_any, int wl,
+                          int sbo, int lr, int coh, int col, float scale, bool prio1) {
   constexpr int WL = 4, WS = 2, TL = 4, BM = 128, NSTAGE = 2;
   constexpr int STAGE = (BM + 256) * kRowB;
+  constexpr int X = MPV_FWD_XFER ? (TSA - TSB) / 2 : 0;
+  constexpr int TSE = X ? (TSA + TSB) / 2 : TSW;  // blocks this wave's epilogue decodes
+  const int lane = threadIdx.x & 63;
   int gs = 0;
   for (int st = t_begin; st < t_end; ++st) {
     const int s0 = fwd_tile_s0<BM>(st, p.S);
@@ -1258,8 +1269,36 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
       fwd16t_mfma<TL, TSW>(acc, f);
     }
     if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
-    fwd_tile_epilogue_t<WL, WS, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                             soft_any, st - t_begin, false, sbo);
+    if (X > 0) {
+      // hand-off of A's last X sample blocks (t of 64 labels x 16 samples each)
+      if (IS_A) {
+#pragma unroll
+        for (int j = 0; j < X; ++j)
+#pragma unroll
+          for (int m = 0; m < TL; ++m)
+            xfer[((wl * X + j) * TL + m) * 64 + lane] = acc[m][TSW - X + j];
+      }
+      lds_barrier();
+      f32x4 e[TL][TSE];
+#pragma unroll
+      for (int m = 0; m < TL; ++m) {
+        if (IS_A) {
+#pragma unroll
+          for (int n = 0; n < TSE; ++n) e[m][n] = acc[m][n];
+        } else {
+#pragma unroll
+          for (int j = 0; j < X; ++j) e[m][j] = xfer[((wl * X + j) * TL + m) * 64 + lane];
+#pragma unroll
+          for (int n = 0; n < TSW; ++n) e[m][X + n] = acc[m][n];
+        }
+      }
+      fwd_tile_epilogue_t<WL, WS, TL, TSE, BM>(p, e, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                               soft_any, st - t_begin, false,
+                                               IS_A ? 0 : TSA - X);
+    } else {
+      fwd_tile_epilogue_t<WL, WS, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                               soft_any, st - t_begin, false, sbo);
+    }
     if (MPV_EPI_PRIO >= 0) {
       if (prio1)
         __builtin_amdgcn_s_setprio(1);
@@ -1276,10 +1315,14 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   static_assert(BM == 128, "the sample tile stays 128");
   constexpr int STAGE = (BM + BN) * kRowB;
   constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN) * 4];
+  constexpr int X = MPV_FWD_XFER ? (TSA - TSB) / 2 : 0;
+  static_assert(!MPV_FWD_XFER || (TSA - TSB) % 2 == 0, "even hand-off");
+  constexpr int XF = WL * X * 4 * 64 * 4;  // floats of the hand-off area
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN + XF) * 4];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red + RED;
   float* cols = cacc + CACC;
+  f32x4* xfer = reinterpret_cast<f32x4*>(cols + 3 * BN);
 
   int g, nt;
   decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
@@ -1316,11 +1359,11 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   const bool prio1 = MPV_FWD_PRIO && dmaw;
   if (prio1) __builtin_amdgcn_s_setprio(1);
   if (wid < NW / 2)
-    fwd16a_tiles<TSA>(p, smem, red, cacc, cols, dma, false, b, nt, t_begin, t_end, nK, soft_any,
-                      wl, 0, lr, coh, col, scale, prio1);
+    fwd16a_tiles<TSA, true, TSA, TSB>(p, smem, red, cacc, cols, xfer, dma, false, b, nt, t_begin,
+                                      t_end, nK, soft_any, wl, 0, lr, coh, col, scale, prio1);
   else
-    fwd16a_tiles<TSB>(p, smem, red, cacc, cols, dma, true, b, nt, t_begin, t_end, nK, soft_any,
-                      wl, TSA, lr, coh, col, scale, prio1);
+    fwd16a_tiles<TSB, false, TSA, TSB>(p, smem, red, cacc, cols, xfer, dma, true, b, nt, t_begin,
+                                       t_end, nK, soft_any, wl, TSA, lr, coh, col, scale, prio1);
   // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
   lds_barrier();
   for (int c = tid; c < BN; c += NW * 64) {
