@@ -588,14 +588,14 @@ MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
     }
 }
 
-// One stage's LDS-DMA for wave wn of group 0: pieces wn*PER_WAVE .. (one row
-// each: the first PIECES/2 are G rows, the rest E rows).
-template <int PER_WAVE, int PIECES>
-MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn, int l0, int z0,
-                       int lane_u, int lane_h) {
+// Pieces pc0 .. pc0+COUNT-1 of one stage's LDS-DMA (one row each: the first
+// PIECES/2 are G rows, the rest E rows).
+template <int COUNT, int PIECES>
+MPV_DEV void drs_issue_range(const Dr16Params& p, char* dst, int q0, int rows, int pc0, int l0,
+                             int z0, int lane_u, int lane_h) {
 #pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    const int pc = wn * PER_WAVE + i;  // wave-uniform
+  for (int i = 0; i < COUNT; ++i) {
+    const int pc = pc0 + i;  // wave-uniform
     const bool is_g = pc < PIECES / 2;
     const int r = is_g ? pc : pc - PIECES / 2;
     const int q = (MPV_ABL & 2048) ? ((q0 & 63) + r) : q0 + r;  // 2048: L2-resident rows (timing study)
@@ -607,6 +607,19 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
     lds_dma16(src, (uint32_t)(((lane_u ^ (r & 7)) << 5) + lane_h), lds_addr(dst + pc * 1024));
   }
 }
+
+// One stage's LDS-DMA for wave wn of group 0: pieces wn*PER_WAVE ...
+template <int PER_WAVE, int PIECES>
+MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn, int l0, int z0,
+                       int lane_u, int lane_h) {
+  drs_issue_range<PER_WAVE, PIECES>(p, dst, q0, rows, wn * PER_WAVE, l0, z0, lane_u, lane_h);
+}
+
+// MPV_DR_G1P: DMA pieces per stage streamed by each group-1 wave (at the start
+// of its MFMA slot, two stages ahead), the rest by group 0 as before.
+#ifndef MPV_DR_G1P
+#define MPV_DR_G1P 0
+#endif
 
 // Staggered schedule: the waves of row wm = 0 (group 0) and wm = 1 (group 1)
 // share the SIMDs pairwise and run one phase apart, so on every SIMD one wave
@@ -629,8 +642,9 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   constexpr int STAGE = 2 * IMG;
   constexpr int PIECES = STAGE / 1024;  // 1-KB wave-instructions per stage
   constexpr int RPP = 1024 / ROWB;      // rows per piece
-  constexpr int PER_WAVE = PIECES / WN; // group 0 streams everything
-  static_assert(PIECES % WN == 0, "DMA pieces must split over group 0");
+  constexpr int G1P = MPV_DR_G1P;                 // pieces per group-1 wave
+  constexpr int PER_WAVE = (PIECES - WN * G1P) / WN;  // pieces per group-0 wave
+  static_assert(PIECES % WN == 0 && G1P <= PIECES / WN, "DMA pieces must split over the waves");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   int kc, tile;
@@ -659,7 +673,8 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
 
   const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
   if (grp == 0 && nst > 0) {
-    drs_issue<PER_WAVE, PIECES>(p, smem, q_begin, rows, wn, l0, z0, lane_u, lane_h);
+    drs_issue_range<PIECES / WN, PIECES>(p, smem, q_begin, rows, wn * (PIECES / WN), l0, z0, lane_u,
+                                         lane_h);
     wait_vmcnt<0>();
   }
   barrier_raw();
@@ -689,20 +704,24 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
     MPV_STAMP(3);                                                                             \
     barrier_raw();                                                                            \
   } while (0)
-#define DR_G1_STAGE(i, PAR)                                                      \
-  do {                                                                           \
-    const int ci = (i);                                                          \
-    (void)ci;                                                                    \
-    MPV_STAMP(0);                                                                \
-    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp); \
-    MPV_STAMP(1);                                                                \
-    lds_barrier();                                                               \
-    MPV_STAMP(2);                                                                \
-    __builtin_amdgcn_s_setprio(1);                                               \
-    dr_mfma<TM, TN>(acc, f);                                                     \
-    __builtin_amdgcn_s_setprio(0);                                               \
-    MPV_STAMP(3);                                                                \
-    barrier_raw();                                                               \
+#define DR_G1_STAGE(i, PAR)                                                        \
+  do {                                                                             \
+    const int ci = (i);                                                            \
+    (void)ci;                                                                      \
+    MPV_STAMP(0);                                                                  \
+    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);   \
+    MPV_STAMP(1);                                                                  \
+    if (G1P) wait_vmcnt<0>(); /* own share of stage (i)+1 landed */                \
+    lds_barrier();                                                                 \
+    MPV_STAMP(2);                                                                  \
+    if (G1P && (i) + 2 < nst) /* stage (i)+2 -> image PAR, read by all by now */   \
+      drs_issue_range<G1P, PIECES>(p, smem + (PAR) * STAGE, q_begin + ((i) + 2) * kDrKR, \
+                                   rows, WN * PER_WAVE + wn * G1P, l0, z0, lane_u, lane_h); \
+    __builtin_amdgcn_s_setprio(1);                                                 \
+    dr_mfma<TM, TN>(acc, f);                                                       \
+    __builtin_amdgcn_s_setprio(0);                                                 \
+    MPV_STAMP(3);                                                                  \
+    barrier_raw();                                                                 \
   } while (0)
   if (grp == 0) {
     // slot 2i: stream stage i+1, read stage i; slot 2i+1: MFMAs of stage i
@@ -719,6 +738,10 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
     }
     barrier_raw();
   } else {
+    // slot 0: group 1's share of stage 1 (image 1 is untouched so far)
+    if (G1P && nst > 1)
+      drs_issue_range<G1P, PIECES>(p, smem + STAGE, q_begin + kDrKR, rows, WN * PER_WAVE + wn * G1P,
+                                   l0, z0, lane_u, lane_h);
     barrier_raw();
     // slot 2i+1: read stage i; slot 2i+2: MFMAs of stage i
     if (MPV_DR_UNROLL2) {
