@@ -139,6 +139,17 @@ def pmc_traffic(config, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def trace_avg_ms(config, kernel):
+    """The committed rocprofv3 trace's average duration of `kernel` over the
+    bench's timed steps (cross-check of the in-library HIP-event timing)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
+    if not files:
+        return None
+    k = json.load(open(files[-1])).get("kernels", {}).get(kernel) or {}
+    return k.get("avg_ms_trace_timed_steps", k.get("avg_ms_trace"))
+
+
 def cpu_baseline(L, z, B, d, S_cpu, reps, device):
     """Reference algorithm restated in torch (oracle/torch_ref.py) on the host
     cores, fwd+bwd on a bounded slice of the workload; also the ELBO rel-err of
@@ -233,6 +244,7 @@ def main():
     value = S_total * B * L * cli.steps / elapsed
     rl = roofline(times, S_local, B, L, z, cli.steps, cli.gemm)
     rl["traffic"], rl["traffic_source"] = pmc_traffic(cli.config, rl["kernel"])
+    rl["rocprof_avg_ms"] = trace_avg_ms(cli.config, rl["kernel"])
 
     cpu, errs = None, None
     if rank == 0 and world == 1 and not cli.no_cpu_baseline:

@@ -56,6 +56,16 @@ def main(src, dst, tag):
         if not r["Name"].startswith(("void mpv::", "mpv::")):
             continue
         dur[k] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6)
+    # per-launch durations in launch order: the timed steps are the last
+    # `timed` launches (bench.py's --steps; the first ones are warm-up)
+    timed = int(os.environ.get("TIMED_STEPS", "10"))
+    per = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_trace.csv"))):
+        if not r["Kernel_Name"].startswith(("void mpv::", "mpv::")):
+            continue
+        per.setdefault(short(r["Kernel_Name"]), []).append(
+            (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    last = {k: [d for _, d in sorted(v)][-timed:] for k, v in per.items()}
     fetch = counters(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = counters(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
     out = {"source": src, "note": "bytes per launch; fetch corrected x2 (gfx950 FETCH_SIZE "
@@ -65,8 +75,10 @@ def main(src, dst, tag):
         hbm = None
         if f_kib is not None and w_kib is not None:
             hbm = (2.0 * f_kib + w_kib) * 1024.0
+        lt = last.get(k) or []
         out["kernels"][k] = {"launches_traced": dur.get(k, (None,))[0],
                              "avg_ms_trace": dur.get(k, (None, None))[1],
+                             "avg_ms_trace_timed_steps": sum(lt) / len(lt) if lt else None,
                              "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                              "hbm_bytes_per_launch": hbm}
     # aliases under the timing tags bench.py reports (e.g. probit_fwd16 -> probit_fwd)

@@ -6,7 +6,8 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${TAG:-c4}"
-ARGS="${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}"
+# the bench's own default step counts (so the trace matches its timed steps)
+ARGS="${BENCH_ARGS:---steps 10 --warmup 3 --no-cpu-baseline}"
 OUT="$R/gpurun_out/prof/$TAG"
 KRE="${KRE:-probit_fwd|dR16|dR_gemm|bwd_elem|noise_philox}"
 mkdir -p "$OUT"
