@@ -165,9 +165,11 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
   f32x2 zq[N], t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    zq[j] = f32x2{fabsf(u[j].x), fabsf(u[j].y)} * (kInvSqrt2 * kSqL2e);
-    const f32x2 den = pk_fma(splat2(0.5f / kSqL2e), zq[j], splat2(1.0f));
-    t[j] = f32x2{fast_rcp(den.x), fast_rcp(den.y)};
+    // zq keeps u's sign: it is used only squared and through |zq|, which the
+    // scalar fma takes as an abs source modifier (no v_and per element)
+    zq[j] = u[j] * (kInvSqrt2 * kSqL2e);
+    t[j] = f32x2{fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].x), 1.0f)),
+                 fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
@@ -200,9 +202,11 @@ MPV_DEV void probit_dE2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phic)[N]) 
   f32x2 zq[N], t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    zq[j] = f32x2{fabsf(u[j].x), fabsf(u[j].y)} * (kInvSqrt2 * kSqL2e);
-    const f32x2 den = pk_fma(splat2(0.5f / kSqL2e), zq[j], splat2(1.0f));
-    t[j] = f32x2{fast_rcp(den.x), fast_rcp(den.y)};
+    // zq keeps u's sign: it is used only squared and through |zq|, which the
+    // scalar fma takes as an abs source modifier (no v_and per element)
+    zq[j] = u[j] * (kInvSqrt2 * kSqL2e);
+    t[j] = f32x2{fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].x), 1.0f)),
+                 fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
