@@ -154,8 +154,15 @@ MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N])
 // into the coefficients, so the exponent is one fma feeding v_exp_f32; the
 // sign of erf follows u by copysign, and 0.5 * C1 is one exact constant.
 // Agrees with probit_eval2 to a few ulps of E.
+//
+// The callers work on w = 1 + erf(u / sqrt 2) = 2 Phi(u): E = kEh w + C0 is
+// one fma that a caller folds into its own affine use of E (q = qa E + qb,
+// the ranking exponent sg E, the column sums), so E is rarely formed at all.
+// 1 + erf is exact for u < 0 (Sterbenz), so a small E keeps its relative
+// precision; folding a rounded 0.5 C1 + C0 into one constant would not.
+constexpr float kEh = 0.5f * kC1;
 template <int N>
-MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
+MPV_DEV void probit_w2xN(const f32x2 (&u)[N], f32x2 (&w)[N]) {
 #pragma clang fp contract(off)
   constexpr float kL2e = 1.4426950408889634f, kSqL2e = 1.2011224087864498f;  // log2 e, sqrt
   constexpr float c[10] = {0.17087277f * kL2e, -0.82215223f * kL2e, 1.48851587f * kL2e,
@@ -182,17 +189,23 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
     const f32x2 a = pk_fma(-zq[j], zq[j], p[j]);
     const f32x2 erfc = t[j] * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
     const f32x2 om = splat2(1.0f) - erfc;
-    const f32x2 onep = splat2(1.0f) + f32x2{__builtin_copysignf(om.x, u[j].x),
-                                            __builtin_copysignf(om.y, u[j].y)};
-    E[j] = onep * (0.5f * kC1) + splat2(kC0);
+    w[j] = splat2(1.0f) +
+           f32x2{__builtin_copysignf(om.x, u[j].x), __builtin_copysignf(om.y, u[j].y)};
   }
 }
 
-// probit_eval2xN for the backward, with the forward's folded constants
-// (probit_prob2xN): E and phic = (1 - 1e-6) phi(u), the factor dE/du needs.
+template <int N>
+MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
+  probit_w2xN<N>(u, E);
+#pragma unroll
+  for (int j = 0; j < N; ++j) E[j] = pk_fma(E[j], splat2(kEh), splat2(kC0));
+}
+
+// probit_w2xN for the backward, with the same folded constants: w
+// (E = kEh w + C0) and phic = (1 - 1e-6) phi(u), the factor dE/du needs.
 // erfc = t * exp(-z^2) * exp(P(t)): exp(-z^2) also gives phi.
 template <int N>
-MPV_DEV void probit_dE2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phic)[N]) {
+MPV_DEV void probit_dw2xN(const f32x2 (&u)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) {
 #pragma clang fp contract(off)
   constexpr float kL2e = 1.4426950408889634f, kSqL2e = 1.2011224087864498f;
   constexpr float c[10] = {0.17087277f * kL2e, -0.82215223f * kL2e, 1.48851587f * kL2e,
@@ -221,9 +234,8 @@ MPV_DEV void probit_dE2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phic)[N]) 
     const f32x2 ep = f32x2{__builtin_amdgcn_exp2f(p[j].x), __builtin_amdgcn_exp2f(p[j].y)};
     phic[j] = ez * (kC1 * kInvSqrt2Pi);
     const f32x2 om = splat2(1.0f) - (t[j] * ez) * ep;
-    const f32x2 onep = splat2(1.0f) + f32x2{__builtin_copysignf(om.x, u[j].x),
-                                            __builtin_copysignf(om.y, u[j].y)};
-    E[j] = onep * (0.5f * kC1) + splat2(kC0);
+    w[j] = splat2(1.0f) +
+           f32x2{__builtin_copysignf(om.x, u[j].x), __builtin_copysignf(om.y, u[j].y)};
   }
 }
 

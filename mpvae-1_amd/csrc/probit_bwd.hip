@@ -117,8 +117,8 @@ struct ElemCol {
   float y[4];
   bool soft[4];
   float sdl[4];   // sign of d logp/dE for a 0/1 label: -1 for y = 0, +1 otherwise
-  float qa[4], qb[4];  // d = qa E + qb: 1 - E for y = 0, E otherwise
-  float sgx[4];   // e^{-5E} (y = 1) or e^{5E}: exponent multiplier in log2 units
+  float qa[4], qb[4];  // d = qa w + qb: 1 - E for y = 0, E otherwise (E = kEh w + C0)
+  float sga[4];   // e^{-5E} (y = 1) or e^{5E} as exp2(sga w) e^{-+5 C0}
   float wp[4], wn[4];  // [y = 1], [y = 0]
 };
 
@@ -126,28 +126,28 @@ struct ElemCol {
 // dependent packed ops of one element interleave with the others'.
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
                        f32x2 (&out)[4]) {
-  f32x2 u[4], E[4], phic[4];
+  f32x2 u[4], w[4], phic[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + c.base[q];
-  probit_dE2xN<4>(u, E, phic);
+  probit_dw2xN<4>(u, w, phic);
   const f32x2 nbP = -bP;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // d logp / dE = y/E - (1-y)/(1-E): one reciprocal of E (y = 1) or 1 - E
-    // (y = 0), selected as qa E + qb
-    const f32x2 d = pk_fma(E[q], splat2(c.qa[q]), splat2(c.qb[q]));
+    // (y = 0), selected as qa w + qb
+    const f32x2 d = pk_fma(w[q], splat2(c.qa[q]), splat2(c.qb[q]));
     const f32x2 r = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
     f32x2 dE;
     if (c.soft[q]) {
-      const f32x2 dl =
-          splat2(c.y[q]) / E[q] - splat2(1.0f - c.y[q]) / (splat2(1.0f) - E[q]);
+      const f32x2 E = pk_fma(w[q], splat2(kEh), splat2(kC0));
+      const f32x2 dl = splat2(c.y[q]) / E - splat2(1.0f - c.y[q]) / (splat2(1.0f) - E);
       dE = pk_fma(alpha, dl, c.gind[q]);
     } else {
       dE = pk_fma(alpha * c.sdl[q], r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
     const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP);
-    const f32x2 a = E[q] * c.sgx[q];
+    const f32x2 a = w[q] * c.sga[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
     out[q] = dE * phic[q];
   }
@@ -227,11 +227,13 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     ec.y[q] = yv[q];
     ec.soft[q] = soft[q];
     ec.sdl[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
-    ec.qa[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
-    ec.qb[q] = yv[q] == 0.0f ? 1.0f : 0.0f;
-    ec.sgx[q] = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
-    ec.wp[q] = yv[q] == 1.0f ? 1.0f : 0.0f;
-    ec.wn[q] = yv[q] == 0.0f ? 1.0f : 0.0f;
+    ec.qa[q] = yv[q] == 0.0f ? -kEh : kEh;  // (1 - E, E) as affine maps of w
+    ec.qb[q] = yv[q] == 0.0f ? 1.0f - kC0 : kC0;
+    const float sgx = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+    ec.sga[q] = sgx * kEh;
+    // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
+    ec.wp[q] = yv[q] == 1.0f ? exp2f(sgx * kC0) : 0.0f;
+    ec.wn[q] = yv[q] == 0.0f ? exp2f(sgx * kC0) : 0.0f;
   }
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);

@@ -911,6 +911,14 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     }
   }
   FWD_ESTAMP2(1);
+  // C0 x (number of this wave's samples that the column sums count)
+  float ecount = 0.0f;
+#pragma unroll
+  for (int n = 0; n < TS; ++n) {
+    const int sb = s0 + (sbo + n) * 16;
+    ecount += (float)max(0, min(S, sb + 16) - max(s_own, sb));
+  }
+  ecount *= kC0;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
 #pragma unroll 1
@@ -954,20 +962,23 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const f32x2 fex[4] = {f32x2{pa[0], pa[1]}, f32x2{pa[2], pa[3]}, f32x2{pb[0], pb[1]},
                           f32x2{pb[2], pb[3]}};
     const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
-    // per label: weights (valid / positive / negative), ranking exponent scale,
-    // and q = qa * E + qb selecting E (y = 1) or 1 - E (y = 0) without a select
-    float wok[4], wpos[4], wneg[4], sg[4], qa[4], qb[4];
+    // per label: weights (valid / positive / negative), the ranking exponent
+    // sg E = sga w + sgb, and q = qa w + qb selecting E (y = 1) or 1 - E
+    // (y = 0) without a select (w = 2 Phi(u), E = kEh w + C0: probit_w2xN)
+    float wok[4], wpos[4], wneg[4], sga[4], sgb[4], qa[4], qb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       wok[i] = n0 + lb + i < L ? 1.0f : 0.0f;
       wpos[i] = y4[i] == 1.0f ? wok[i] : 0.0f;
       wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
-      sg[i] = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
-      // q = qa * E + qb: E (y = 1), 1 - E (y = 0), 1 (pad label or soft label,
-      // whose two-log BCE term is added separately)
+      const float sg = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
+      sga[i] = sg * kEh;
+      sgb[i] = sg * kC0;
+      // q: E (y = 1), 1 - E (y = 0), 1 (pad label or soft label, whose
+      // two-log BCE term is added separately)
       const bool hard = wok[i] != 0.0f && (y4[i] == 0.0f || y4[i] == 1.0f);
-      qa[i] = !hard ? 0.0f : (y4[i] == 0.0f ? -1.0f : 1.0f);
-      qb[i] = !hard ? 1.0f : (y4[i] == 0.0f ? 1.0f : 0.0f);
+      qa[i] = !hard ? 0.0f : (y4[i] == 0.0f ? -kEh : kEh);
+      qb[i] = !hard ? 1.0f : (y4[i] == 0.0f ? 1.0f - kC0 : kC0);
     }
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
@@ -975,22 +986,22 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       const int s = s0 + (sbo + n) * 16 + lr;
       const float wr = (s >= s_own && s < S) ? 1.0f : 0.0f;
       const f32x4 t4 = am[n];
-      f32x2 uu[4], E4[4];
+      f32x2 uu[4], w4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + fex[i];
       if (MPV_ABL & 4096) {  // timing study: no probit
 #pragma unroll
-        for (int i = 0; i < 4; ++i) E4[i] = uu[i] * 0.01f + splat2(0.5f);
+        for (int i = 0; i < 4; ++i) w4[i] = uu[i] * 0.01f + splat2(1.0f);
       } else {
-        probit_prob2xN<4>(uu, E4);
+        probit_w2xN<4>(uu, w4);
       }
       f32x2 q[4], r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // BCE operand (mpvae.py:184-185): E for y = 1, 1 - E for y = 0, 1 for a pad label
-        q[i] = pk_fma(E4[i], splat2(qa[i]), splat2(qb[i]));
+        q[i] = pk_fma(w4[i], splat2(qa[i]), splat2(qb[i]));
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-        const f32x2 a = E4[i] * sg[i];
+        const f32x2 a = pk_fma(w4[i], splat2(sga[i]), splat2(sgb[i]));
         r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       }
       // sum of the 4 labels' log-probs as ONE log of their product (log2 units,
@@ -1003,7 +1014,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         for (int i = 0; i < 4; ++i) {
           const float y = y4[i];
           if (wok[i] != 0.0f && !(y == 0.0f || y == 1.0f)) {  // soft label: both BCE terms (q = 1)
-            const f32x2 E = E4[i];
+            const f32x2 E = pk_fma(w4[i], splat2(kEh), splat2(kC0));
             lp.x += y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
             lp.y += y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
           }
@@ -1015,7 +1026,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       for (int i = 0; i < 4; ++i) {
         sp[n] = pk_fma(splat2(wpos[i]), r[i], sp[n]);
         sn[n] = pk_fma(splat2(wneg[i]), r[i], sn[n]);
-        ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);
+        ce[i] = pk_fma(splat2(wr), w4[i], ce[i]);  // sum E = kEh sum w + C0 count
       }
       // MPV_EPI_SB samples at a time: bounded live ranges vs more independent chains
       if (MPV_EPI_SB > 0 && (n + 1) % MPV_EPI_SB == 0) __builtin_amdgcn_sched_barrier(0);
@@ -1031,8 +1042,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
       if (lr == 15) {
         float* c = cacc + (ws * BN + lb + i) * 2;
-        c[0] += e;
-        c[1] += x;
+        c[0] += fmaf(kEh, e, ecount);
+        c[1] += fmaf(kEh, x, ecount);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
