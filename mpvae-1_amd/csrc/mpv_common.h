@@ -161,27 +161,38 @@ MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N])
 // 1 + erf is exact for u < 0 (Sterbenz), so a small E keeps its relative
 // precision; folding a rounded 0.5 C1 + C0 into one constant would not.
 constexpr float kEh = 0.5f * kC1;
+//
+// P(t) here is a degree-7 minimax fit of log(erfc(z) / t) + z^2 over
+// t >= 0.35 (|u| <= 5.3; tools/fit_erfc.py) in place of the degree-9
+// Numerical Recipes fit over all t: below t = 0.35 its error grows, but there
+// erfc(z) < 1.2e-7 and E = C0 + C1 Phi(u) is C0-dominated, so E's relative
+// error stays at the fp32 rounding of zq^2 that bounds both fits (2.5e-6 at
+// |u| ~ 5, emulated in fp32 over |u| <= 40 by tools/fit_erfc.py: the same
+// maximum as NR's).  Two fewer packed fmas per element pair.
+//
+// zq = u sqrt(log2 e) / sqrt 2 is the caller's: it keeps u's sign (used only
+// squared, through |zq| as an fma abs source modifier, and for erf's sign),
+// and a caller with u = t + base forms it as one fma(t, kZq, base kZq).
+constexpr int kErfcDeg = 7;
+constexpr float kSqL2e = 1.2011224087864498f;  // sqrt(log2 e)
+constexpr float kZq = kInvSqrt2 * kSqL2e;
 template <int N>
-MPV_DEV void probit_w2xN(const f32x2 (&u)[N], f32x2 (&w)[N]) {
+MPV_DEV void probit_w2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N]) {
 #pragma clang fp contract(off)
-  constexpr float kL2e = 1.4426950408889634f, kSqL2e = 1.2011224087864498f;  // log2 e, sqrt
-  constexpr float c[10] = {0.17087277f * kL2e, -0.82215223f * kL2e, 1.48851587f * kL2e,
-                           -1.13520398f * kL2e, 0.27886807f * kL2e, -0.18628806f * kL2e,
-                           0.09678418f * kL2e, 0.37409196f * kL2e, 1.00002368f * kL2e,
-                           -1.26551223f * kL2e};
-  f32x2 zq[N], t[N], p[N];
+  constexpr float kL2e = 1.4426950408889634f;  // log2 e
+  constexpr float c[kErfcDeg + 1] = {
+      -0.106683437f * kL2e, 0.374139153f * kL2e, -0.264585754f * kL2e, -0.429977846f * kL2e,
+      0.443629564f * kL2e,  0.218868934f * kL2e, 1.03288951f * kL2e,   -1.26828029f * kL2e};
+  f32x2 t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    // zq keeps u's sign: it is used only squared and through |zq|, which the
-    // scalar fma takes as an abs source modifier (no v_and per element)
-    zq[j] = u[j] * (kInvSqrt2 * kSqL2e);
     t[j] = f32x2{fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].x), 1.0f)),
                  fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
 #pragma unroll
-  for (int k = 2; k < 10; ++k)
+  for (int k = 2; k <= kErfcDeg; ++k)
 #pragma unroll
     for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], p[j], splat2(c[k]));
 #pragma unroll
@@ -190,41 +201,40 @@ MPV_DEV void probit_w2xN(const f32x2 (&u)[N], f32x2 (&w)[N]) {
     const f32x2 erfc = t[j] * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
     const f32x2 om = splat2(1.0f) - erfc;
     w[j] = splat2(1.0f) +
-           f32x2{__builtin_copysignf(om.x, u[j].x), __builtin_copysignf(om.y, u[j].y)};
+           f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};
   }
 }
 
 template <int N>
 MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
-  probit_w2xN<N>(u, E);
+  f32x2 zq[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) zq[j] = u[j] * kZq;
+  probit_w2xN_zq<N>(zq, E);
 #pragma unroll
   for (int j = 0; j < N; ++j) E[j] = pk_fma(E[j], splat2(kEh), splat2(kC0));
 }
 
-// probit_w2xN for the backward, with the same folded constants: w
+// probit_w2xN_zq for the backward, with the same folded constants: w
 // (E = kEh w + C0) and phic = (1 - 1e-6) phi(u), the factor dE/du needs.
 // erfc = t * exp(-z^2) * exp(P(t)): exp(-z^2) also gives phi.
 template <int N>
-MPV_DEV void probit_dw2xN(const f32x2 (&u)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) {
+MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) {
 #pragma clang fp contract(off)
-  constexpr float kL2e = 1.4426950408889634f, kSqL2e = 1.2011224087864498f;
-  constexpr float c[10] = {0.17087277f * kL2e, -0.82215223f * kL2e, 1.48851587f * kL2e,
-                           -1.13520398f * kL2e, 0.27886807f * kL2e, -0.18628806f * kL2e,
-                           0.09678418f * kL2e, 0.37409196f * kL2e, 1.00002368f * kL2e,
-                           -1.26551223f * kL2e};
-  f32x2 zq[N], t[N], p[N];
+  constexpr float kL2e = 1.4426950408889634f;
+  constexpr float c[kErfcDeg + 1] = {
+      -0.106683437f * kL2e, 0.374139153f * kL2e, -0.264585754f * kL2e, -0.429977846f * kL2e,
+      0.443629564f * kL2e,  0.218868934f * kL2e, 1.03288951f * kL2e,   -1.26828029f * kL2e};
+  f32x2 t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    // zq keeps u's sign: it is used only squared and through |zq|, which the
-    // scalar fma takes as an abs source modifier (no v_and per element)
-    zq[j] = u[j] * (kInvSqrt2 * kSqL2e);
     t[j] = f32x2{fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].x), 1.0f)),
                  fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
 #pragma unroll
-  for (int k = 2; k < 10; ++k)
+  for (int k = 2; k <= kErfcDeg; ++k)
 #pragma unroll
     for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], p[j], splat2(c[k]));
 #pragma unroll
@@ -235,7 +245,7 @@ MPV_DEV void probit_dw2xN(const f32x2 (&u)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) 
     phic[j] = ez * (kC1 * kInvSqrt2Pi);
     const f32x2 om = splat2(1.0f) - (t[j] * ez) * ep;
     w[j] = splat2(1.0f) +
-           f32x2{__builtin_copysignf(om.x, u[j].x), __builtin_copysignf(om.y, u[j].y)};
+           f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};
   }
 }
 

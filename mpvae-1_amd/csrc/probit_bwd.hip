@@ -112,7 +112,7 @@ struct ElemParams {
 // (mpvae.py:110-117, 184-185 differentiated), dL/dt = dE (1-1e-6) phi(u).
 // Per-column constants of the element pass (the lane's four label columns).
 struct ElemCol {
-  f32x2 base[4];  // fe_out, fx_out
+  f32x2 base[4];  // fe_out, fx_out, in the probit's argument units (x kZq)
   f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total
   float y[4];
   bool soft[4];
@@ -126,10 +126,10 @@ struct ElemCol {
 // dependent packed ops of one element interleave with the others'.
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
                        f32x2 (&out)[4]) {
-  f32x2 u[4], w[4], phic[4];
+  f32x2 zq[4], w[4], phic[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) u[q] = splat2(t[q]) + c.base[q];
-  probit_dw2xN<4>(u, w, phic);
+  for (int q = 0; q < 4; ++q) zq[q] = pk_fma(splat2(t[q]), splat2(kZq), c.base[q]);
+  probit_dw2xN_zq<4>(zq, w, phic);
   const f32x2 nbP = -bP;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
   ElemCol ec;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    ec.base[q] = f32x2{fe[q], fx[q]};
+    ec.base[q] = f32x2{fe[q], fx[q]} * kZq;
     ec.gind[q] = f32x2{gil[q], gi[q]};
     ec.y[q] = yv[q];
     ec.soft[q] = soft[q];

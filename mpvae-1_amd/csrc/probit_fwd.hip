@@ -247,8 +247,9 @@ MPV_DEV void fwd_cols_stage_t(float* cols, const FwdParams& p, int b, int n0, in
     const int col = n0 + i;
     const bool ok = col < p.L;
     const int64_t o = (int64_t)b * p.L + (ok ? col : 0);
-    cols[2 * i] = ok ? p.fe[o] : 0.0f;
-    cols[2 * i + 1] = ok ? p.fx[o] : 0.0f;
+    // pre-scaled to the probit's argument units: zq = fma(t, kZq, fe kZq)
+    cols[2 * i] = ok ? p.fe[o] * kZq : 0.0f;
+    cols[2 * i + 1] = ok ? p.fx[o] * kZq : 0.0f;
     cols[2 * BN + i] = ok ? p.y[o] : 0.0f;
   }
 }
@@ -964,7 +965,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
     // per label: weights (valid / positive / negative), the ranking exponent
     // sg E = sga w + sgb, and q = qa w + qb selecting E (y = 1) or 1 - E
-    // (y = 0) without a select (w = 2 Phi(u), E = kEh w + C0: probit_w2xN)
+    // (y = 0) without a select (w = 2 Phi(u), E = kEh w + C0: probit_w2xN_zq)
     float wok[4], wpos[4], wneg[4], sga[4], sgb[4], qa[4], qb[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -986,14 +987,14 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       const int s = s0 + (sbo + n) * 16 + lr;
       const float wr = (s >= s_own && s < S) ? 1.0f : 0.0f;
       const f32x4 t4 = am[n];
-      f32x2 uu[4], w4[4];
+      f32x2 zq[4], w4[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) uu[i] = splat2(t4[i]) + fex[i];
+      for (int i = 0; i < 4; ++i) zq[i] = pk_fma(splat2(t4[i]), splat2(kZq), fex[i]);
       if (MPV_ABL & 4096) {  // timing study: no probit
 #pragma unroll
-        for (int i = 0; i < 4; ++i) w4[i] = uu[i] * 0.01f + splat2(1.0f);
+        for (int i = 0; i < 4; ++i) w4[i] = zq[i] * 0.01f + splat2(1.0f);
       } else {
-        probit_w2xN<4>(uu, w4);
+        probit_w2xN_zq<4>(zq, w4);
       }
       f32x2 q[4], r[4];
 #pragma unroll
