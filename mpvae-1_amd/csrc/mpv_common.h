@@ -162,18 +162,18 @@ MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N])
 // precision; folding a rounded 0.5 C1 + C0 into one constant would not.
 constexpr float kEh = 0.5f * kC1;
 //
-// P(t) here is a degree-7 minimax fit of log(erfc(z) / t) + z^2 over
-// t >= 0.35 (|u| <= 5.3; tools/fit_erfc.py) in place of the degree-9
-// Numerical Recipes fit over all t: below t = 0.35 its error grows, but there
-// erfc(z) < 1.2e-7 and E = C0 + C1 Phi(u) is C0-dominated, so E's relative
-// error stays at the fp32 rounding of zq^2 that bounds both fits (2.5e-6 at
-// |u| ~ 5, emulated in fp32 over |u| <= 40 by tools/fit_erfc.py: the same
-// maximum as NR's).  Two fewer packed fmas per element pair.
+// P(t) here is a degree-6 minimax fit of log(erfc(z) / t) + z^2 over
+// t >= 0.38 (|u| <= 4.6; tools/fit_erfc.py) in place of the degree-9
+// Numerical Recipes fit over all t: below t = 0.38 its error grows, but there
+// erfc(z) < 6e-6 and E = C0 + C1 Phi(u) is soon C0-dominated.  Emulated in
+// fp32 over |u| <= 40, E's maximum relative error is 2.6e-6 against NR's
+// 2.46e-6; both are set by the fp32 rounding of zq^2 near |u| ~ 5, not by P.
+// Three fewer packed fmas per element pair.
 //
 // zq = u sqrt(log2 e) / sqrt 2 is the caller's: it keeps u's sign (used only
 // squared, through |zq| as an fma abs source modifier, and for erf's sign),
 // and a caller with u = t + base forms it as one fma(t, kZq, base kZq).
-constexpr int kErfcDeg = 7;
+constexpr int kErfcDeg = 6;
 constexpr float kSqL2e = 1.2011224087864498f;  // sqrt(log2 e)
 constexpr float kZq = kInvSqrt2 * kSqL2e;
 template <int N>
@@ -181,8 +181,8 @@ MPV_DEV void probit_w2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N]) {
 #pragma clang fp contract(off)
   constexpr float kL2e = 1.4426950408889634f;  // log2 e
   constexpr float c[kErfcDeg + 1] = {
-      -0.106683437f * kL2e, 0.374139153f * kL2e, -0.264585754f * kL2e, -0.429977846f * kL2e,
-      0.443629564f * kL2e,  0.218868934f * kL2e, 1.03288951f * kL2e,   -1.26828029f * kL2e};
+      -0.139353514f * kL2e, 0.777093824f * kL2e, -1.58356997f * kL2e, 1.19629222f * kL2e,
+      -0.0702797193f * kL2e, 1.09342452f * kL2e, -1.27360696f * kL2e};
   f32x2 t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -223,8 +223,8 @@ MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&phic)[
 #pragma clang fp contract(off)
   constexpr float kL2e = 1.4426950408889634f;
   constexpr float c[kErfcDeg + 1] = {
-      -0.106683437f * kL2e, 0.374139153f * kL2e, -0.264585754f * kL2e, -0.429977846f * kL2e,
-      0.443629564f * kL2e,  0.218868934f * kL2e, 1.03288951f * kL2e,   -1.26828029f * kL2e};
+      -0.139353514f * kL2e, 0.777093824f * kL2e, -1.58356997f * kL2e, 1.19629222f * kL2e,
+      -0.0702797193f * kL2e, 1.09342452f * kL2e, -1.27360696f * kL2e};
   f32x2 t[N], p[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {

@@ -6,7 +6,7 @@ toward the minimax error, then emulates the kernel's fp32 evaluation (folded
 log2 e constants, one rounding per fma) and reports E's relative error over
 |u| <= 40 next to the degree-9 Numerical Recipes fit the kernels used before.
 
-usage: python tools/fit_erfc.py [deg tmin]      (default: 7 0.35)
+usage: python tools/fit_erfc.py [deg tmin]      (default: 6 0.38, the kernels' fit)
 """
 import sys
 
@@ -59,8 +59,8 @@ def kernel_erfc(u, coef):
 
 
 def main():
-    deg = int(sys.argv[1]) if len(sys.argv) > 1 else 7
-    tmin = float(sys.argv[2]) if len(sys.argv) > 2 else 0.35
+    deg = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    tmin = float(sys.argv[2]) if len(sys.argv) > 2 else 0.38
     coef = fit(deg, tmin)
     c1, c0 = float(f32(1 - 1e-6)), float(f32(0.5e-6))
     u = np.linspace(0, 40, 800001)  # E at -u (the small side)
