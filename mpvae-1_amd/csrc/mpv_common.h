@@ -215,35 +215,37 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
   for (int j = 0; j < N; ++j) E[j] = pk_fma(E[j], splat2(kEh), splat2(kC0));
 }
 
-// probit_w2xN_zq for the backward, with the same folded constants: w
-// (E = kEh w + C0) and phic = (1 - 1e-6) phi(u), the factor dE/du needs.
-// erfc = t * exp(-z^2) * exp(P(t)): exp(-z^2) also gives phi.
+// probit_w2xN_zq for the backward: w (E = kEh w + C0) and phic =
+// (1 - 1e-6) phi(u), the factor dE/du needs.  exp(-z^2) gives phi, so erfc
+// is taken as t exp(-z^2) Q(t) with Q a degree-6 minimax fit of
+// erfcx(z) / t over t >= 0.38 (relative; tools/fit_erfc.py, form q) instead
+// of a second exponential of P(t).  fp32-emulated E error over |u| <= 40:
+// max 2.4e-6 (the forward's P form 2.6e-6, NR 2.46e-6).
+constexpr int kErfcxDeg = 6;
 template <int N>
 MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) {
 #pragma clang fp contract(off)
-  constexpr float kL2e = 1.4426950408889634f;
-  constexpr float c[kErfcDeg + 1] = {
-      -0.139353514f * kL2e, 0.777093824f * kL2e, -1.58356997f * kL2e, 1.19629222f * kL2e,
-      -0.0702797193f * kL2e, 1.09342452f * kL2e, -1.27360696f * kL2e};
-  f32x2 t[N], p[N];
+  constexpr float c[kErfcxDeg + 1] = {0.0899837102f, -0.359859836f, 0.38748431f,
+                                      0.0453561664f, 0.275197459f,  0.279788422f,
+                                      0.282049996f};
+  f32x2 t[N], q[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     t[j] = f32x2{fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].x), 1.0f)),
                  fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
-  for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
 #pragma unroll
-  for (int k = 2; k <= kErfcDeg; ++k)
+  for (int k = 2; k <= kErfcxDeg; ++k)
 #pragma unroll
-    for (int j = 0; j < N; ++j) p[j] = pk_fma(t[j], p[j], splat2(c[k]));
+    for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], q[j], splat2(c[k]));
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const f32x2 az = -zq[j] * zq[j];
     const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
-    const f32x2 ep = f32x2{__builtin_amdgcn_exp2f(p[j].x), __builtin_amdgcn_exp2f(p[j].y)};
     phic[j] = ez * (kC1 * kInvSqrt2Pi);
-    const f32x2 om = splat2(1.0f) - (t[j] * ez) * ep;
+    const f32x2 om = splat2(1.0f) - (t[j] * ez) * q[j];
     w[j] = splat2(1.0f) +
            f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};
   }
