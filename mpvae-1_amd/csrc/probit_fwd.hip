@@ -98,6 +98,9 @@ struct FwdParams {
 #ifndef MPV_FWD_TSA
 #define MPV_FWD_TSA 5
 #endif
+#ifndef MPV_FWD_LOAD
+#define MPV_FWD_LOAD 0  // study: 4 loader waves stream a ring of MPV_FWD_LOAD stages (probit_fwd16L)
+#endif
 #ifndef MPV_FWD_XFER
 #define MPV_FWD_XFER 0  // rebalance the asymmetric forward's epilogue through LDS (study: +1 %)
 #endif
@@ -1393,6 +1396,147 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   }
 }
 
+// ------------------------- 3xf16 with loader waves (probit_fwd16L, study)
+// probit_fwd16t's 256 x 128 tile (8 compute waves of 64 x 64) plus 4 loader
+// waves that only stream the stage images: the DMA issue (48 LDS-DMA pieces
+// per stage, ~100+ cycles each) leaves the compute waves' MFMA chain, and a
+// ring of NSTAGE images lets the loaders run NSTAGE-1 stages ahead (with 3,
+// the epilogue's row-sum area lives in the image the tile's last stage read).
+// The loaders mirror every barrier of the compute waves: one per K stage and
+// three in each tile's epilogue.  12 waves = 3 per SIMD caps the kernel at
+// 168 VGPRs.
+constexpr int kFwdLoaders = 4;
+
+template <int NSTAGE>
+MPV_DEV void fwd16L_compute(const FwdParams& p, char* smem, float* red_own, float* cacc,
+                            const float* cols, int b, int nt, int t_begin, int t_end, int nK,
+                            bool soft_any, int wl, int sbo, int lr, int coh, int col,
+                            float scale) {
+  constexpr int WL = 4, WS = 2, TL = 4, TS = 4, BM = 128;
+  constexpr int STAGE = (BM + 256) * kRowB;
+  constexpr bool RED_IN_RING = NSTAGE >= 3;
+  int gs = 0;
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TS];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
+      // no vmcnt wait: this wave's only vector-memory ops are its T / row stores
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed (loaders waited); every wave is done reading gs-1
+      FragT<TL, TS> f;
+      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+      fwd16t_mfma<TL, TS>(acc, f);
+    }
+    if (MPV_ABL & 1) {  // timing study: no epilogue (the loaders' barriers still matched)
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 512 + threadIdx.x] = v;
+      if (RED_IN_RING) barrier_raw();
+      barrier_raw();
+      barrier_raw();
+      continue;
+    }
+    float* red = RED_IN_RING
+                     ? reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE)
+                     : red_own;
+    fwd_tile_epilogue_t<WL, WS, TL, TS, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                             soft_any, st - t_begin, RED_IN_RING, sbo);
+  }
+}
+
+template <int NSTAGE>
+__global__ __launch_bounds__(768, 1) void probit_fwd16L_kernel(FwdParams p) {
+  constexpr int WL = 4, WS = 2, NC = 8, NW = NC + kFwdLoaders;
+  constexpr int BM = 128, BN = 256;
+  constexpr int STAGE = (BM + BN) * kRowB;
+  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
+  constexpr bool RED_IN_RING = NSTAGE >= 3;
+  static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
+  constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + 3 * BN) * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED_OWN;
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL;
+  const int lr = lane & 15, lg = lane >> 4;
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  bool my_soft = false;
+  for (int i = tid; i < BN; i += NW * 64) {
+    const int l = n0 + i;
+    if (l < p.L) {
+      const float yv = p.y[(int64_t)b * p.L + l];
+      my_soft |= !(yv == 0.0f || yv == 1.0f);
+    }
+  }
+  const bool soft_any = __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
+  if (wid >= NC) {
+    using Dma = Fwd16Dma<BM, BN, kFwdLoaders>;
+    static_assert(Dma::EVEN, "every loader streams the same piece count");
+    constexpr int PW = Dma::JA + Dma::JB;  // pieces per loader wave per stage
+    Dma dma;
+    dma.init(p, t_begin, b, n0, wid - NC, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+    int gs = 0;
+    for (int st = t_begin; st < t_end; ++st) {
+      for (int kc = 0; kc < nK; ++kc, ++gs) {
+        // stage gs landed: leave the younger issued stages in flight
+        if (NSTAGE >= 3 && dma.issued >= gs + 2)
+          wait_vmcnt<(NSTAGE >= 3 ? PW : 0)>();
+        else
+          wait_vmcnt<0>();
+        barrier_raw();
+        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
+                  t_end, nK, b);
+      }
+      // the epilogue's barriers: red-in-ring hand-over, then the row statistics
+      if (RED_IN_RING) barrier_raw();
+      barrier_raw();
+      barrier_raw();
+    }
+  } else {
+    fwd16L_compute<NSTAGE>(p, smem, red, cacc, cols, b, nt, t_begin, t_end, nK, soft_any, wl,
+                           (wid / WL) * 4, lr, coh, col, scale);
+  }
+  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
+  lds_barrier();
+  for (int c = tid; c < BN; c += NW * 64) {
+    const int l = n0 + c;
+    if (l < p.L) {
+      float e = 0.f, x = 0.f;
+#pragma unroll
+      for (int w = 0; w < WS; ++w) {
+        e += cacc[(w * BN + c) * 2 + 0];
+        x += cacc[(w * BN + c) * 2 + 1];
+      }
+      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + l] = e;
+      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + l] = x;
+    }
+  }
+}
+
 // --------------------- 3xf16, epilogue pipelined into the next tile (fwd16p)
 // probit_fwd16t with the epilogue of tile i run INSIDE the K loop of tile
 // i+1, by the same waves: in probit_fwd16t every wave reaches the epilogue
@@ -1877,7 +2021,9 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         if (MPV_FWD_BIG)  // 256 labels x 256 samples, 8 waves of 128 x 64
           MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
         else
-          if (MPV_FWD_TSA != 4)
+          if (MPV_FWD_LOAD)
+            MPV_LAUNCH("probit_fwd", probit_fwd16L_kernel<MPV_FWD_LOAD>, grid, dim3(768), 0, st, p);
+          else if (MPV_FWD_TSA != 4)
             MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<MPV_FWD_TSA, 8 - MPV_FWD_TSA>), grid,
                        dim3(512), 0, st, p);
           else
