@@ -98,6 +98,9 @@ struct FwdParams {
 #ifndef MPV_FWD_TSA
 #define MPV_FWD_TSA 5
 #endif
+#ifndef MPV_FWD_PF
+#define MPV_FWD_PF 0  // study: fragments prefetched one stage ahead in registers (probit_fwd16a)
+#endif
 #ifndef MPV_FWD_LOAD
 #define MPV_FWD_LOAD 0  // study: 4 loader waves stream a ring of MPV_FWD_LOAD stages (probit_fwd16L)
 #endif
@@ -1272,16 +1275,44 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
     for (int m = 0; m < TL; ++m)
 #pragma unroll
       for (int n = 0; n < TSW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nK; ++kc, ++gs) {
-      wait_vmcnt<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-      if (dmaw)
-        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
-                  t_end, nK, b);
-      FragT<TL, TSW> f;
-      fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
-      fwd16t_mfma<TL, TSW>(acc, f);
+    if (MPV_FWD_PF) {
+      // fragments one stage ahead in registers: the MFMAs of stage gs start
+      // right after the barrier while stage gs+1's fragments are read.
+      // Stage g sits in slot g % 2 and is issued two stages ahead (at the
+      // barrier of g-2, into the slot whose fragments are already held).
+      FragT<TL, TSW> f0, f1;
+      // stage gs landed before the previous stage's barrier (or the prologue's)
+      fwd16t_read<WL, TL, TSW, BM>(f0, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+      auto step = [&](FragT<TL, TSW>& cur, FragT<TL, TSW>& nxt, bool pf) {
+        wait_vmcnt<0>();  // DMA waves: stage gs+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // cur is in registers
+        barrier_raw();
+        if (dmaw)
+          dma.issue(p, smem + (__builtin_amdgcn_readfirstlane(gs) % NSTAGE) * STAGE, t_end, nK, b);
+        if (pf)
+          fwd16t_read<WL, TL, TSW, BM>(nxt, smem + ((gs + 1) % NSTAGE) * STAGE, wl, sbo, lr, coh,
+                                       col);
+        fwd16t_mfma<TL, TSW>(acc, cur);
+        ++gs;
+      };
+      int kc = 0;
+      for (; kc + 1 < nK; kc += 2) {
+        step(f0, f1, true);
+        step(f1, f0, kc + 2 < nK);
+      }
+      if (kc < nK) step(f0, f1, false);
+    } else {
+      for (int kc = 0; kc < nK; ++kc, ++gs) {
+        wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+        if (dmaw)
+          dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
+                    t_end, nK, b);
+        FragT<TL, TSW> f;
+        fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+        fwd16t_mfma<TL, TSW>(acc, f);
+      }
     }
     if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
     if (X > 0) {
@@ -1369,7 +1400,12 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   dma.init(p, t_begin, b, n0, wid % (NW / 2), lane);
   if (dmaw) {
 #pragma unroll
-    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+    for (int j = 0; j < (MPV_FWD_PF ? NSTAGE : NSTAGE - 1); ++j)
+      dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+  if (MPV_FWD_PF) {  // stage 0 (and 1) landed before the first tile's fragment read
+    wait_vmcnt<0>();
+    barrier_raw();
   }
   const bool prio1 = MPV_FWD_PRIO && dmaw;
   if (prio1) __builtin_amdgcn_s_setprio(1);
@@ -2023,7 +2059,7 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
         else
           if (MPV_FWD_LOAD)
             MPV_LAUNCH("probit_fwd", probit_fwd16L_kernel<MPV_FWD_LOAD>, grid, dim3(768), 0, st, p);
-          else if (MPV_FWD_TSA != 4)
+          else if (MPV_FWD_TSA != 4 || MPV_FWD_PF)
             MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<MPV_FWD_TSA, 8 - MPV_FWD_TSA>), grid,
                        dim3(512), 0, st, p);
           else
