@@ -116,8 +116,7 @@ struct ElemCol {
   f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total
   float y[4];
   bool soft[4];
-  float sdl[4];   // sign of d logp/dE for a 0/1 label: -1 for y = 0, +1 otherwise
-  float qa[4], qb[4];  // d = qa w + qb: 1 - E for y = 0, E otherwise (E = kEh w + C0)
+  float qb[4];  // d = kEh w + qb: E - 1 for y = 0 (the sign of d logp/dE folded in), E otherwise
   float sga[4];   // e^{-5E} (y = 1) or e^{5E} as exp2(sga w) e^{-+5 C0}
   float wp[4], wn[4];  // [y = 1], [y = 0]
 };
@@ -133,9 +132,9 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
   const f32x2 nbP = -bP;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    // d logp / dE = y/E - (1-y)/(1-E): one reciprocal of E (y = 1) or 1 - E
-    // (y = 0), selected as qa w + qb
-    const f32x2 d = pk_fma(w[q], splat2(c.qa[q]), splat2(c.qb[q]));
+    // d logp / dE = y/E - (1-y)/(1-E): one reciprocal of E (y = 1) or of
+    // E - 1 (y = 0, the sign folded in), selected as kEh w + qb
+    const f32x2 d = pk_fma(w[q], splat2(kEh), splat2(c.qb[q]));
     const f32x2 r = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
     f32x2 dE;
     if (c.soft[q]) {
@@ -143,7 +142,7 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
       const f32x2 dl = splat2(c.y[q]) / E - splat2(1.0f - c.y[q]) / (splat2(1.0f) - E);
       dE = pk_fma(alpha, dl, c.gind[q]);
     } else {
-      dE = pk_fma(alpha * c.sdl[q], r, c.gind[q]);
+      dE = pk_fma(alpha, r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
     const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP);
@@ -226,9 +225,7 @@ __global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
     ec.gind[q] = f32x2{gil[q], gi[q]};
     ec.y[q] = yv[q];
     ec.soft[q] = soft[q];
-    ec.sdl[q] = yv[q] == 0.0f ? -1.0f : 1.0f;
-    ec.qa[q] = yv[q] == 0.0f ? -kEh : kEh;  // (1 - E, E) as affine maps of w
-    ec.qb[q] = yv[q] == 0.0f ? 1.0f - kC0 : kC0;
+    ec.qb[q] = yv[q] == 0.0f ? kC0 - 1.0f : kC0;  // E - 1 = -(1 - E), E: affine maps of w
     const float sgx = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
     ec.sga[q] = sgx * kEh;
     // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
