@@ -294,6 +294,21 @@ MPV_DEV float row16_sum_to_lane15(float v) {
   return v;
 }
 
+// row16_sum_to_lane15 of N values step-major: the N independent chains fill
+// each other's DPP wait states (no s_nop), and with the permuted operand as
+// src0 the add and the row shift fuse into one v_add_f32_dpp.
+template <int N>
+MPV_DEV void row16_sum_to_lane15_n(float (&v)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = dpp_f<0x111>(v[j]) + v[j];
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = dpp_f<0x112>(v[j]) + v[j];
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = dpp_f<0x114>(v[j]) + v[j];
+#pragma unroll
+  for (int j = 0; j < N; ++j) v[j] = dpp_f<0x118>(v[j]) + v[j];
+}
+
 // Sum over the four 16-lane rows of the wave (lanes l, l^16, l^32, l^48) by
 // the gfx950 row-swap permutes (VALU, no LDS): every lane gets the total.
 MPV_DEV float sum_lanegroups(float v) {

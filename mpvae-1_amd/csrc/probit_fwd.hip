@@ -1038,19 +1038,22 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       // MPV_EPI_SB samples at a time: bounded live ranges vs more independent chains
       if (MPV_EPI_SB > 0 && (n + 1) % MPV_EPI_SB == 0) __builtin_amdgcn_sched_barrier(0);
     }
-    // column sums of these 4 labels over the wave's samples: 16-lane trees,
-    // lane 15 of each row accumulates into the (ws, label) slot it owns
+    // column sums of these 4 labels over the wave's samples: 16-lane trees
+    // (8 chains step-major), lane 15 of each row accumulates into the
+    // (ws, label) slot it owns
+    float cs[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (MPV_ABL & 8192) {
-        if (lr == 15) cacc[(ws * BN + lb + i) * 2] += ce[i].x + ce[i].y;
-        continue;
-      }
-      const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
-      if (lr == 15) {
+      cs[2 * i] = ce[i].x;
+      cs[2 * i + 1] = ce[i].y;
+    }
+    row16_sum_to_lane15_n<8>(cs);
+    if (lr == 15) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
         float* c = cacc + (ws * BN + lb + i) * 2;
-        c[0] += fmaf(kEh, e, ecount);
-        c[1] += fmaf(kEh, x, ecount);
+        c[0] += fmaf(kEh, cs[2 * i], ecount);
+        c[1] += fmaf(kEh, cs[2 * i + 1], ecount);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
