@@ -320,6 +320,24 @@ MPV_DEV float sum_lanegroups(float v) {
   return __uint_as_float(c[0]) + __uint_as_float(c[1]);
 }
 
+// sum_lanegroups of N values step-major (independent chains between the
+// permutes instead of wait states).
+template <int N>
+MPV_DEV void sum_lanegroups_n(float (&v)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j]),
+                                                    false, false);
+    v[j] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j]),
+                                                    false, false);
+    v[j] = __uint_as_float(c[0]) + __uint_as_float(c[1]);
+  }
+}
+
 MPV_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);

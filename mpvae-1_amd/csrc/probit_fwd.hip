@@ -1062,15 +1062,23 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // red in a ring image: every wave must be past its last fragment read of it
   if (sync_before_red) lds_barrier();
   // row statistics: sum over the 4 lane rows; lanes of row 0 publish
+  float v[TS * 6];
 #pragma unroll
   for (int n = 0; n < TS; ++n) {
     sl[n] = sl[n] * 0.6931471805599453f;  // rows outside the tile's own range are not published
-    const float v[6] = {sl[n].x, sl[n].y, sp[n].x, sn[n].x, sp[n].y, sn[n].y};
+    v[n * 6 + 0] = sl[n].x;
+    v[n * 6 + 1] = sl[n].y;
+    v[n * 6 + 2] = sp[n].x;
+    v[n * 6 + 3] = sn[n].x;
+    v[n * 6 + 4] = sp[n].y;
+    v[n * 6 + 5] = sn[n].y;
+  }
+  sum_lanegroups_n<TS * 6>(v);  // all chains step-major
+  if (lg == 0) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const float tot = sum_lanegroups(v[k]);
-      if (lg == 0) red[(wl * BM + (sbo + n) * 16 + lr) * 6 + k] = tot;
-    }
+    for (int n = 0; n < TS; ++n)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) red[(wl * BM + (sbo + n) * 16 + lr) * 6 + k] = v[n * 6 + k];
   }
   FWD_ESTAMP2(3);
   lds_barrier();
