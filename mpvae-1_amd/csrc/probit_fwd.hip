@@ -98,6 +98,9 @@ struct FwdParams {
 #ifndef MPV_FWD_TSA
 #define MPV_FWD_TSA 5
 #endif
+#ifndef MPV_EPI_UNROLL
+#define MPV_EPI_UNROLL 1  // label groups per epilogue loop iteration (1: rotate by one)
+#endif
 #ifndef MPV_FWD_PF
 #define MPV_FWD_PF 0  // study: fragments prefetched one stage ahead in registers (probit_fwd16a)
 #endif
@@ -928,15 +931,23 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   ecount *= kC0;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
+  // MPV_EPI_UNROLL = U groups per (not unrolled) iteration, the accumulators
+  // rotating down by U after it: fewer register moves, U x the code
+  constexpr int EU = (MPV_EPI_UNROLL > 1 && TL % MPV_EPI_UNROLL == 0) ? MPV_EPI_UNROLL : 1;
 #pragma unroll 1
-  for (int m = 0; m < TL; ++m) {
+  for (int mp = 0; mp < TL; mp += EU) {
+#pragma unroll
+  for (int h = 0; h < EU; ++h) {
+    const int m = mp + h;
     f32x4 am[TS];
 #pragma unroll
-    for (int n = 0; n < TS; ++n) am[n] = acc[0][n];
+    for (int n = 0; n < TS; ++n) am[n] = acc[h][n];
+    if (h == EU - 1) {  // rotate the remaining groups down
 #pragma unroll
-    for (int mm = 0; mm + 1 < TL; ++mm)
+      for (int mm = 0; mm + EU < TL; ++mm)
 #pragma unroll
-      for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + 1][n];
+        for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + EU][n];
+    }
     const int lb = (wl * TL + m) * 16 + lg * 4;  // first of the lane's 4 labels in the tile
     if (MPV_EPI_ALT) {
       // the two waves of a SIMD take turns at priority, one label group
@@ -1057,6 +1068,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
+  }
   }
   FWD_ESTAMP2(2);
   // red in a ring image: every wave must be past its last fragment read of it
