@@ -249,17 +249,33 @@ MPV_DEV void fwd_cols_stage(float* cols, const FwdParams& p, int b, int n0, int 
   }
 }
 
-// The transposed kernel's layout: colsT[2*BN] = (fe, fx) pairs, then y[BN].
+// The transposed kernel's layout (kColsT * BN floats): (fe, fx) pairs, then
+// y[BN], then the epilogue's per-label constants, one BN array each (so a
+// lane reads its 4 labels' values as one f32x4): qa, qb (q = qa w + qb: E for
+// y = 1, 1 - E for y = 0, 1 for a pad or soft label), sga, sgb (ranking
+// exponent sg E = sga w + sgb), wpos, wneg ([y = 1], [y = 0] of a real label).
+// Staged once per workgroup: the labels are the same for all its tiles.
+constexpr int kColsT = 9;
+enum { kCqa = 3, kCqb, kCsga, kCsgb, kCwpos, kCwneg };
 template <int BN>
 MPV_DEV void fwd_cols_stage_t(float* cols, const FwdParams& p, int b, int n0, int nthreads) {
   for (int i = threadIdx.x; i < BN; i += nthreads) {
     const int col = n0 + i;
     const bool ok = col < p.L;
     const int64_t o = (int64_t)b * p.L + (ok ? col : 0);
+    const float y = ok ? p.y[o] : 0.0f;
     // pre-scaled to the probit's argument units: zq = fma(t, kZq, fe kZq)
     cols[2 * i] = ok ? p.fe[o] * kZq : 0.0f;
     cols[2 * i + 1] = ok ? p.fx[o] * kZq : 0.0f;
-    cols[2 * BN + i] = ok ? p.y[o] : 0.0f;
+    cols[2 * BN + i] = y;
+    const float sg = y == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
+    const bool hard = ok && (y == 0.0f || y == 1.0f);
+    cols[kCqa * BN + i] = !hard ? 0.0f : (y == 0.0f ? -kEh : kEh);
+    cols[kCqb * BN + i] = !hard ? 1.0f : (y == 0.0f ? 1.0f - kC0 : kC0);
+    cols[kCsga * BN + i] = sg * kEh;
+    cols[kCsgb * BN + i] = sg * kC0;
+    cols[kCwpos * BN + i] = (ok && y == 1.0f) ? 1.0f : 0.0f;
+    cols[kCwneg * BN + i] = (ok && y == 0.0f) ? 1.0f : 0.0f;
   }
 }
 
@@ -980,24 +996,16 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const f32x2 fex[4] = {f32x2{pa[0], pa[1]}, f32x2{pa[2], pa[3]}, f32x2{pb[0], pb[1]},
                           f32x2{pb[2], pb[3]}};
     const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
-    // per label: weights (valid / positive / negative), the ranking exponent
-    // sg E = sga w + sgb, and q = qa w + qb selecting E (y = 1) or 1 - E
-    // (y = 0) without a select (w = 2 Phi(u), E = kEh w + C0: probit_w2xN_zq)
-    float wok[4], wpos[4], wneg[4], sga[4], sgb[4], qa[4], qb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wok[i] = n0 + lb + i < L ? 1.0f : 0.0f;
-      wpos[i] = y4[i] == 1.0f ? wok[i] : 0.0f;
-      wneg[i] = y4[i] == 0.0f ? wok[i] : 0.0f;
-      const float sg = y4[i] == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
-      sga[i] = sg * kEh;
-      sgb[i] = sg * kC0;
-      // q: E (y = 1), 1 - E (y = 0), 1 (pad label or soft label, whose
-      // two-log BCE term is added separately)
-      const bool hard = wok[i] != 0.0f && (y4[i] == 0.0f || y4[i] == 1.0f);
-      qa[i] = !hard ? 0.0f : (y4[i] == 0.0f ? -kEh : kEh);
-      qb[i] = !hard ? 1.0f : (y4[i] == 0.0f ? 1.0f - kC0 : kC0);
-    }
+    // per label: the ranking exponent sg E = sga w + sgb, q = qa w + qb
+    // selecting E (y = 1) or 1 - E (y = 0) without a select, and the
+    // positive / negative weights (w = 2 Phi(u), E = kEh w + C0:
+    // probit_w2xN_zq), staged per workgroup by fwd_cols_stage_t
+    const f32x4 qa = *reinterpret_cast<const f32x4*>(cols + kCqa * BN + lb);
+    const f32x4 qb = *reinterpret_cast<const f32x4*>(cols + kCqb * BN + lb);
+    const f32x4 sga = *reinterpret_cast<const f32x4*>(cols + kCsga * BN + lb);
+    const f32x4 sgb = *reinterpret_cast<const f32x4*>(cols + kCsgb * BN + lb);
+    const f32x4 wpos = *reinterpret_cast<const f32x4*>(cols + kCwpos * BN + lb);
+    const f32x4 wneg = *reinterpret_cast<const f32x4*>(cols + kCwneg * BN + lb);
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
@@ -1031,7 +1039,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float y = y4[i];
-          if (wok[i] != 0.0f && !(y == 0.0f || y == 1.0f)) {  // soft label: both BCE terms (q = 1)
+          if (n0 + lb + i < L && !(y == 0.0f || y == 1.0f)) {  // soft label: both BCE terms (q = 1)
             const f32x2 E = pk_fma(w4[i], splat2(kEh), splat2(kC0));
             lp.x += y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
             lp.y += y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
@@ -1122,7 +1130,7 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   constexpr bool RED_IN_RING = NSTAGE >= 3;
   static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
   constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + 3 * BN) * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + kColsT * BN) * 4];
   float* red_own = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red_own + RED_OWN;
   float* cols = cacc + CACC;
@@ -1387,11 +1395,11 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   constexpr int X = MPV_FWD_XFER ? (TSA - TSB) / 2 : 0;
   static_assert(!MPV_FWD_XFER || (TSA - TSB) % 2 == 0, "even hand-off");
   constexpr int XF = WL * X * 4 * 64 * 4;  // floats of the hand-off area
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + 3 * BN + XF) * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN + XF) * 4];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red + RED;
   float* cols = cacc + CACC;
-  f32x4* xfer = reinterpret_cast<f32x4*>(cols + 3 * BN);
+  f32x4* xfer = reinterpret_cast<f32x4*>(cols + kColsT * BN);
 
   int g, nt;
   decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
@@ -1519,7 +1527,7 @@ __global__ __launch_bounds__(768, 1) void probit_fwd16L_kernel(FwdParams p) {
   constexpr bool RED_IN_RING = NSTAGE >= 3;
   static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
   constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + 3 * BN) * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + kColsT * BN) * 4];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red + RED_OWN;
   float* cols = cacc + CACC;
