@@ -470,7 +470,10 @@ MPV_DEV u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    // a ^ b ^ k as one v_bitop3_b32 (truth table 0x96); the compiler emits two
+    // v_xor_b32 for the plain expression
+    c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+              (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
