@@ -157,6 +157,9 @@ def _noise_source(args, n_sample, B, z, shard, device):
         seed = getattr(args, "mpvae_seed", None)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if shard.exchange is not None:
+            # one noise stream for the whole job: rank 0's seed (mpvae_dist.py)
+            seed = shard.exchange.agree_seed(seed, device)
         return None, dict(noise="philox", seed=seed, offset=0)
     raise ValueError(f"unknown args.mpvae_noise {mode!r} (torch_cpu | philox | tensor)")
 

@@ -20,17 +20,79 @@ needed.  With philox noise, element ((s*B+b)*z+k) of the noise is a function
 of its global index only, so the sharded run draws exactly the single-device
 noise.  The collectives go through torch.distributed: RCCL ("nccl") over xGMI
 on the GPU node, gloo for the CPU tests.
+
+Replica contract.  Every rank must hold the same y / fe_out / fx_out /
+r_sqrt_sigma (same batch, same dropout masks, same reparameterisation draws:
+seed torch and numpy identically on every rank) -- otherwise the combined
+statistics mix different forward graphs and the MLP replicas drift apart
+silently.  Two guards:
+  * the Philox seed is broadcast from the group's rank 0 (agree_seed), so a
+    per-rank seed (the common seed + rank pattern) cannot split the noise;
+  * verify_replicas compares an order-sensitive fp64 checksum of those four
+    tensors across ranks (all_reduce MIN and MAX) and raises ReplicaMismatch
+    on every rank when they differ.  It costs one host sync, so it runs on the
+    first sharded compute_loss of the process and then only when
+    args.mpvae_check_replicas is True (False disables it entirely).
 """
 import torch
 import torch.distributed as dist
 
 
+class ReplicaMismatch(RuntimeError):
+    """Ranks of a sample-sharded compute_loss hold different inputs."""
+
+
+_FIRST_CALL_CHECKED = False
+
+
+def replica_checksum(tensors):
+    """(2 * len(tensors),) fp64 checksum: plain sum and a position-weighted sum
+    of each tensor (identical tensors give bitwise identical checksums on
+    identical devices; a permutation or a single changed element does not)."""
+    out = []
+    for t in tensors:
+        x = t.detach().reshape(-1).to(torch.float64)
+        w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.float64)
+        w = torch.remainder(w * 0.6180339887498949, 1.0) + 0.5
+        out += [x.sum(), (x * w).sum()]
+    return torch.stack(out)
+
+
 class SampleShardExchange:
     """Exact cross-rank combine of the per-shard statistics and gradients."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, verify=False):
         self.group = group
         self.world = dist.get_world_size(group)
+        self.verify = verify
+
+    def _src(self):
+        return 0 if self.group is None else dist.get_global_rank(self.group, 0)
+
+    def agree_seed(self, seed, device):
+        """The Philox seed of the group's rank 0, on every rank."""
+        u = int(seed) & (2 ** 64 - 1)  # the 64-bit Philox key, carried as int64
+        t = torch.tensor([u - 2 ** 64 if u >= 2 ** 63 else u], dtype=torch.int64, device=device)
+        dist.broadcast(t, src=self._src(), group=self.group)
+        return int(t.item()) & (2 ** 64 - 1)
+
+    def verify_replicas(self, tensors):
+        """Raise ReplicaMismatch (on every rank) unless all ranks hold the same
+        tensors.  No-op unless this exchange was built with verify=True."""
+        if not self.verify:
+            return
+        ck = replica_checksum(tensors)
+        lo, hi = ck.clone(), ck.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        if not torch.equal(lo, hi):
+            bad = [i // 2 for i in range(ck.numel()) if float(lo[i]) != float(hi[i])]
+            names = ["input_label", "fe_out", "fx_out", "r_sqrt_sigma"]
+            raise ReplicaMismatch(
+                "sample-sharded compute_loss: ranks hold different "
+                + ", ".join(sorted({names[i] if i < len(names) else str(i) for i in bad}))
+                + " -- seed torch and numpy identically on every rank (same batch, "
+                  "dropout masks and reparameterisation draws)")
 
     def combine(self, bstat, colsum, backend):
         parts = [torch.empty_like(bstat) for _ in range(self.world)]
@@ -60,7 +122,10 @@ def split_samples(n_sample, world, rank):
 def shard_for(args, n_sample, group=None):
     """This rank's slice of the sample axis (the whole axis unless args.mpvae_shard).
     args.mpvae_force_exchange runs the collectives even on a world of one (a
-    rehearsal of the multi-GPU path on a single GPU)."""
+    rehearsal of the multi-GPU path on a single GPU).  args.mpvae_check_replicas:
+    None (default) verifies the replica contract on the first sharded call of
+    the process, True on every call, False never."""
+    global _FIRST_CALL_CHECKED
     if not getattr(args, "mpvae_shard", False) or not dist.is_available() \
             or not dist.is_initialized():
         return Shard(n_sample, 0, None)
@@ -70,4 +135,7 @@ def shard_for(args, n_sample, group=None):
     if n_sample < world:
         raise ValueError(f"n_sample={n_sample} cannot be sharded over {world} ranks")
     S_local, s_offset = split_samples(n_sample, world, rank)
-    return Shard(S_local, s_offset, SampleShardExchange(group))
+    check = getattr(args, "mpvae_check_replicas", None)
+    verify = bool(check) if check is not None else not _FIRST_CALL_CHECKED
+    _FIRST_CALL_CHECKED = True
+    return Shard(S_local, s_offset, SampleShardExchange(group, verify=verify))

@@ -201,6 +201,9 @@ class LocalExchange:
     """Single shard: global statistics are the local ones."""
     world = 1
 
+    def verify_replicas(self, tensors):
+        pass
+
     def combine(self, bstat, colsum, backend):
         return bstat, colsum
 
@@ -236,6 +239,7 @@ class ProbitELBO(torch.autograd.Function):
         if R.dim() != 2 or R.shape[0] != L:
             raise ValueError(f"r_sqrt_sigma must be (label_dim={L}, z_dim), got {tuple(R.shape)}")
         z = R.shape[1]
+        cfg.exchange.verify_replicas((y, fe_out, fx_out, R))
         shape = be.shape(cfg.S_local, cfg.S_total, cfg.s_offset, B, L, z)
         if cfg.noise == "philox":
             eps = be.make_noise(shape, y.device, cfg.seed, cfg.offset)

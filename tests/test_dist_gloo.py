@@ -78,3 +78,55 @@ def test_split_samples_covers_axis():
         parts = [split_samples(n, w, r) for r in range(w)]
         assert sum(p[0] for p in parts) == n
         assert [p[1] for p in parts] == list(np.cumsum([0] + [p[0] for p in parts])[:-1])
+
+
+def _replica_worker(rank, world, port, q):
+    """Rank-dependent fe_out must raise ReplicaMismatch on every rank; the
+    Philox seed is rank 0's whatever each rank proposes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golden_io import fixtures
+        from mpvae_dist import ReplicaMismatch
+        from oracle_backend import OracleShardBackend
+        f = next(f for f in fixtures() if f.name == "f1_l38")
+        ex = SampleShardExchange(verify=True)
+        seeds = (ex.agree_seed(1000 + rank, "cpu"), ex.agree_seed(2 ** 64 - 1 - rank, "cpu"))
+        S_local, s_off = split_samples(f.S, world, rank)
+        t = {k: torch.from_numpy(f[k].copy()) for k in
+             ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar",
+              "r_sqrt_sigma"]}
+        noise = torch.from_numpy(f["noise"][s_off:s_off + S_local].copy())
+        outcome = []
+        for perturb in (False, True):
+            fe = t["fe_out"].clone()
+            if perturb and rank == world - 1:
+                fe[0, 0] += 1e-3   # one element on one rank
+            cfg = ElboConfig(f.S, S_local, s_off, f.nll_coeff, f.c_coeff,
+                             backend=OracleShardBackend(), exchange=ex)
+            try:
+                ProbitELBO.apply(t["y"], fe, t["fe_mu"], t["fe_logvar"], t["fx_out"], t["fx_mu"],
+                                 t["fx_logvar"], t["r_sqrt_sigma"], noise, cfg)
+                outcome.append("ok")
+            except ReplicaMismatch as e:
+                outcome.append("mismatch" if "fe_out" in str(e) else str(e))
+        q.put((rank, seeds, outcome))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replica_contract_is_enforced():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, seeds, outcome in results:
+        assert seeds == (1000, 2 ** 64 - 1), (rank, seeds)
+        assert outcome == ["ok", "mismatch"], (rank, outcome)
