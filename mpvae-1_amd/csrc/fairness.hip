@@ -12,8 +12,11 @@
 //                          weighted means of indiv_prob_label / indiv_prob over
 //                          the batch and over each sensitive group, l1 or l2
 //                          distance, summed over target labels and groups.  fp64
-//                          throughout, as in the reference (its weights tensor
-//                          is float64, so the products promote).  Also stashes
+//                          throughout.  The reference computes in fp64 when its
+//                          distances are numpy float64 (torch.tensor(weights)
+//                          is float64 and the products promote) and in fp32
+//                          when they are Python floats; the host returns the
+//                          loss in that dtype (mpvae_fair.py).  Also stashes
 //                          f'(d) / W_tk and sum_k f'(d) / W_t for the backward.
 //   fair_bwd_kernel        d penalty / d indiv_prob[_label] (autograd through
 //                          the same lines; |x|' = sgn(x), sgn(0) = 0).

@@ -16,6 +16,14 @@ host fallback.  Differences from the reference, none of them numeric:
   active (and then does not add it); ``fairness_penalty`` returns a zero
   fp64 tensor instead, which adds nothing -- deciding "float or tensor" would
   need a host sync every step;
+* the penalty is computed in fp64 whatever the distance values are.  The
+  reference's ``torch.tensor(weights)`` is float64 when the dict values are
+  numpy float64 (label_distance*.py's ``np.clip(np.exp(...))``) and float32
+  when they are Python floats (indication / constant / un-gamma'd Jaccard and
+  Hamming), and the penalty then runs in fp32.  The returned loss takes the
+  reference's dtype (fp32 when every table holds Python floats), its value
+  differs from the reference's fp32 one by fp32 rounding only
+  (tests/golden fair_f6/f7, tests/test_gpu_fair.py);
 * the metrics come back as 0-d fp64 device tensors (``.item()`` works as on
   the reference's numpy scalars); p@k ties go to the larger label index
   (numpy's default argsort is not stable, so the reference's tie order is
@@ -66,6 +74,10 @@ class LabelDistanceTable:
 
     def __init__(self, distances, label_dim, device):
         self.L, self.W = label_dim, (label_dim + 63) // 64
+        # torch.tensor() of the looked-up values is float64 iff they are numpy
+        # float64 (fairsoft_train.py:91-97); Python floats give float32
+        self.ref_dtype = torch.float64 if any(isinstance(v, np.float64)
+                                              for v in distances.values()) else torch.float32
         items = [(pack_pattern(k, label_dim), float(v)) for k, v in distances.items()]
         items = [(w, v) for w, v in items if w is not None]
         n = 1
@@ -161,8 +173,10 @@ def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, 
     sensitive_feat                -- (B, n_sensitive) (data.sensitive_feat[idx])
     tables                        -- [LabelDistanceTable(label_distances[t], L, dev)
                                       for t in target_fair_labels]
-    Returns ``(fairloss, contributed)``: fairloss is a differentiable 0-d fp64
-    tensor to add to total_loss (zero when no term is active), contributed the
+    Returns ``(fairloss, contributed)``: fairloss is a differentiable 0-d
+    tensor to add to total_loss (zero when no term is active), computed in fp64
+    and returned in the reference's dtype (fp64 if any table holds numpy
+    float64 distances, else fp32), contributed the
     int32 count that the reference adds to contributed_reg_fair_sample."""
     H.require_gpu(indiv_prob_label, indiv_prob, input_label, sensitive_feat)
     w, count = label_weights(input_label, tables)
@@ -170,6 +184,8 @@ def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, 
     norm = NORMS.get(fairness_loss_norm, 0)
     loss = _FairPenalty.apply(indiv_prob_label, indiv_prob, w, gid, order, goff, G, norm,
                               fair_coeff)
+    if all(t.ref_dtype == torch.float32 for t in tables):
+        loss = loss.float()
     return loss, count
 
 

@@ -15,6 +15,11 @@ def fair_fixtures():
         d = {k: z[k] for k in z.files}
         d["name"] = os.path.basename(p)[5:-4]
         d["dists"] = json.loads(str(d["dists"]))
+        # the value types decide the reference's weights dtype (make_golden_fair.py):
+        # np.float64 -> float64, Python float -> float32
+        d["pyfloat"] = bool(int(d["pyfloat"])) if "pyfloat" in d else False
+        if not d["pyfloat"]:
+            d["dists"] = [{k: np.float64(v) for k, v in t.items()} for t in d["dists"]]
         d["norm"] = str(d["norm"])
         d["coeff"] = float(d["coeff"])
         out.append(d)

@@ -52,7 +52,7 @@ class _Data:
     pass
 
 
-def run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed):
+def run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed, pyfloat=False):
     rng = np.random.default_rng(seed)
     B, L = labels.shape
     lz = torch.tensor(rng.uniform(0.01, 0.99, (B, L)), dtype=torch.float32, requires_grad=True)
@@ -71,7 +71,8 @@ def run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed):
                sensitive=sens, norm=np.array(norm), coeff=np.array(coeff),
                contributed=np.array(ns["contributed_reg_fair_sample"]),
                dists=np.array(json.dumps([{k: float(v) for k, v in dists[t].items()}
-                                          for t in targets])))
+                                          for t in targets])),
+               pyfloat=np.array(int(pyfloat)))
     if isinstance(fl, float):
         rec["active"] = np.array(0)
         rec["fairloss"] = np.array(fl)
@@ -79,13 +80,14 @@ def run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed):
         fl.backward()
         rec["active"] = np.array(1)
         rec["fairloss"] = np.array(fl.item())
+        rec["ref_dtype"] = np.array(str(fl.dtype).replace("torch.", ""))
         rec["g_label_z"] = lz.grad.numpy()
         rec["g_feat_z"] = fz.grad.numpy()
         rec["total"] = np.array(ns["total_loss"].item())
     return rec
 
 
-def make_dists(rng, labels, n_targets, n_extra, miss_rows=0):
+def make_dists(rng, labels, n_targets, n_extra, miss_rows=0, pyfloat=False):
     B, L = labels.shape
     keys = ["".join(r.astype(str)) for r in labels[miss_rows:]]
     extra = ["".join(rng.integers(0, 2, L).astype(str)) for _ in range(n_extra)]
@@ -94,7 +96,14 @@ def make_dists(rng, labels, n_targets, n_extra, miss_rows=0):
         tk = "".join(rng.integers(0, 2, L).astype(str))
         # np.float64 values, as label_distance.py's np.clip(np.exp(...)) produces:
         # the reference's torch.tensor(weights) is then float64
-        d = {k: np.float64(rng.uniform(0.05, 1.0)) for k in keys + extra if rng.random() < 0.7}
+        # pyfloat: Python floats, as label_distance_obs.py's indication (1.0 / 0.),
+        # constant (1.0), and un-gamma'd Jaccard / Hamming (int / int) produce:
+        # torch.tensor(weights) is then float32 and the whole penalty runs in fp32
+        if pyfloat:
+            d = {k: int(rng.integers(0, 4)) / 3 for k in keys + extra if rng.random() < 0.7}
+        else:
+            d = {k: np.float64(rng.uniform(0.05, 1.0)) for k in keys + extra
+                 if rng.random() < 0.7}
         dists[tk] = d
         targets.append(tk)
     return dists, targets
@@ -103,14 +112,16 @@ def make_dists(rng, labels, n_targets, n_extra, miss_rows=0):
 def main():
     block, (a, b) = fairness_block()
     print(f"fairness block: fairsoft_train.py:{a}-{b}")
-    cases = [  # name, B, L, n_sens_cols, n_targets, norm, coeff, seed, miss_rows
-        ("f1_l1", 16, 12, 2, 2, "l1", 1.5, 1, 0),
-        ("f2_l2", 16, 12, 2, 2, "l2", 0.7, 2, 0),
-        ("f3_zero_group", 24, 20, 1, 3, "l1", 2.0, 3, 8),
-        ("f4_l100", 32, 100, 2, 2, "l2", 1.0, 4, 0),
-        ("f5_inactive", 8, 10, 1, 1, "l1", 1.0, 5, 8),
+    cases = [  # name, B, L, n_sens_cols, n_targets, norm, coeff, seed, miss_rows, pyfloat
+        ("f1_l1", 16, 12, 2, 2, "l1", 1.5, 1, 0, False),
+        ("f2_l2", 16, 12, 2, 2, "l2", 0.7, 2, 0, False),
+        ("f3_zero_group", 24, 20, 1, 3, "l1", 2.0, 3, 8, False),
+        ("f4_l100", 32, 100, 2, 2, "l2", 1.0, 4, 0, False),
+        ("f5_inactive", 8, 10, 1, 1, "l1", 1.0, 5, 8, False),
+        ("f6_pyfloat_l1", 64, 24, 2, 2, "l1", 1.5, 6, 4, True),
+        ("f7_pyfloat_l2", 64, 90, 2, 3, "l2", 0.8, 7, 0, True),
     ]
-    for name, B, L, ns_, T, norm, coeff, seed, miss in cases:
+    for name, B, L, ns_, T, norm, coeff, seed, miss, pyf in cases:
         rng = np.random.default_rng(100 + seed)
         labels = (rng.random((B, L)) < 0.3).astype(np.int64)
         labels[B // 2:, :] = labels[:B - B // 2, :]  # repeated patterns
@@ -118,10 +129,11 @@ def main():
         if name == "f3_zero_group":
             sens[:8, 0] = 5  # a group whose rows (the first 8) are all absent from the dicts
         dists, targets = make_dists(rng, labels, T, 4, miss_rows=miss if name != "f5_inactive"
-                                    else B)
-        rec = run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed)
+                                    else B, pyfloat=pyf)
+        rec = run_fair_case(block, labels, sens, dists, targets, norm, coeff, seed, pyfloat=pyf)
         np.savez(os.path.join(HERE, f"fair_{name}.npz"), **rec)
         print(name, "active", int(rec["active"]), "fairloss", float(rec["fairloss"]),
+              str(rec.get("ref_dtype", "-")),
               "contributed", int(rec["contributed"]))
 
     ev = load_evals()

@@ -37,11 +37,19 @@ def test_fair_penalty_matches_reference(f):
         assert float(loss) == 0.0 and float(gl.abs().max()) == 0.0
         return
     ref = float(f["fairloss"])
-    assert loss.dtype == torch.float64
-    assert abs(float(loss) - ref) <= 1e-12 * abs(ref)
-    for g, r in ((gl, f["g_label_z"]), (gf, f["g_feat_z"])):
+    assert str(loss.dtype) == "torch." + str(f["ref_dtype"])
+    if f["pyfloat"]:
+        # the reference ran in fp32 (Python-float distances), the kernels in fp64
+        ltol, gtol = 1e-7, 1e-6
+    else:
         # fp64 on both sides, fp32 at the leaf: a few fp32 ulps
-        assert np.abs(g.cpu().numpy() - r).max() <= 1e-6 * np.abs(r).max()
+        ltol, gtol = 1e-12, 1e-6
+    # a fp32 loss carries the fp64 value rounded once
+    if loss.dtype == torch.float32:
+        ltol = max(ltol, 1.2e-7)
+    assert abs(float(loss) - ref) <= ltol * abs(ref)
+    for g, r in ((gl, f["g_label_z"]), (gf, f["g_feat_z"])):
+        assert np.abs(g.cpu().numpy() - r).max() <= gtol * np.abs(r).max()
 
 
 @pytest.mark.parametrize("norm", ["l1", "l2"])

@@ -138,10 +138,10 @@ RANDOM_CASES = [
 ]
 
 
-@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
-@pytest.mark.parametrize("L,z,B,S,d", RANDOM_CASES)
-def test_random_against_oracle(L, z, B, S, d, gemm):
-    rng = np.random.default_rng(L * 7 + S)
+def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed):
+    """(forward errors, gradient errors) of the HIP path vs oracle.probit_elbo on
+    seeded random inputs with explicit noise."""
+    rng = np.random.default_rng(seed)
     y = (rng.random((B, L)) < 0.25).astype(np.float32)
     y[:, 0], y[:, 1] = 1, 0
     f32 = lambda a: a.astype(np.float32)
@@ -152,26 +152,51 @@ def test_random_against_oracle(L, z, B, S, d, gemm):
     noise = f32(rng.standard_normal((S, B, z)))
     g_I, g_IL = f32(rng.standard_normal((B, L))), f32(rng.standard_normal((B, L)))
     ref = pe.elbo_forward(inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"], inp["fx_out"],
-                          inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, 0.5, 10.0)
+                          inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, nll_coeff,
+                          c_coeff)
     rg = pe.elbo_backward(ref, inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"],
-                          inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, 0.5, 10.0,
+                          inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, nll_coeff, c_coeff,
                           g_total=1.0, g_I=g_I, g_IL=g_IL)
     t = {k: torch.from_numpy(v).to(DEV) for k, v in inp.items()}
     for k in DIFF + ["r_sqrt_sigma"]:
         t[k].requires_grad_(True)
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
-                              mode="train", nll_coeff=0.5, c_coeff=10.0,
+                              mode="train", nll_coeff=nll_coeff, c_coeff=c_coeff,
                               mpvae_noise=torch.from_numpy(noise), mpvae_gemm=gemm)
     out = _call(t, args)
-    for k, o in zip(OUTS, out):
-        assert rel_err(_np(o), ref[k]) <= FWD_RTOL, (k, rel_err(_np(o), ref[k]))
+    ferr = {k: rel_err(_np(o), ref[k]) for k, o in zip(OUTS, out)}
     obj = out[0] + (out[6] * torch.from_numpy(g_I).to(DEV)).sum() + \
         (out[7] * torch.from_numpy(g_IL).to(DEV)).sum()
     obj.backward()
+    gerr = {k: rel_err(_np(t[k].grad), rg[k]) for k in DIFF + ["r_sqrt_sigma"]}
+    return ferr, gerr
+
+
+@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
+@pytest.mark.parametrize("L,z,B,S,d", RANDOM_CASES)
+def test_random_against_oracle(L, z, B, S, d, gemm):
+    ferr, gerr = _against_oracle(L, z, B, S, d, gemm, 0.5, 10.0, L * 7 + S)
+    for k, e in ferr.items():
+        assert e <= FWD_RTOL, (k, e)
     gtol = LONG_K_GRAD_RTOL if z >= 2048 else GRAD_RTOL
-    for k in DIFF + ["r_sqrt_sigma"]:
-        e = rel_err(_np(t[k].grad), rg[k])
+    for k, e in gerr.items():
         assert e <= gtol, (k, e)
+
+
+@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
+def test_headline_coefficients_against_oracle(gemm):
+    """The bench's own coefficients (nll_coeff 0.1, c_coeff 200: main.py:58,62)
+    at the headline L = z = 1024 with a realistic batch (B = 64) and small S,
+    against the fp64-reduction oracle at the stated tolerances.  (bench.py's
+    elbo_rel_err compares with the torch-CPU restatement instead, whose fp32
+    1 - E near E -> 1 moves d fe_out by ~2e-3: tests/test_oracle_golden.py
+    pins that spread.)"""
+    ferr, gerr = _against_oracle(1024, 1024, 64, 16, 50, gemm, 0.1, 200.0, 2024)
+    print(gemm, "fwd", ferr, "grad", gerr)
+    for k, e in ferr.items():
+        assert e <= FWD_RTOL, (k, e)
+    for k, e in gerr.items():
+        assert e <= GRAD_RTOL, (k, e)
 
 
 def test_shard_invariance_at_c4_size():
@@ -208,6 +233,55 @@ def test_shard_invariance_at_c4_size():
         assert rel_err(_np(o2), _np(o1)) <= 1e-5, k
     p = _np(out_full[6])
     assert (p > 0).all() and (p < 1).all()
+
+
+def test_backward_shard_invariance_at_c4_size():
+    """The backward kernels with S_local < S_total and s_offset > 0:
+    two ragged S-shards (1500 + 2596 samples) each run backward_local with the
+    combined global bstat; their packed [d fe_out | d fx_out | dR] buffers
+    summed (what the rank all_reduce does) equal the unsharded backward."""
+    B, S, L, z = 512, 4096, 1024, 1024
+    g = torch.Generator(device=DEV).manual_seed(4)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
+         * (6.0 / (L + z)) ** 0.5)
+    g_I = torch.randn((B, L), device=DEV, generator=g)
+    g_IL = torch.randn((B, L), device=DEV, generator=g)
+    # g_total, g_nll, g_nll_x, g_c, g_c_x (g_kl does not reach these kernels)
+    gscal = torch.tensor([1.0, 0.3, 0.2, 0.7, 0.4, 0.0], device=DEV)
+    live = 0b011111
+    be = HipShardBackend()
+    Rop = be.prepare_R(R)
+    seed = 13572468
+
+    def fwd(S_loc, s_off):
+        shape = be.shape(S_loc, S, s_off, B, L, z)
+        eps = be.make_noise(shape, DEV, seed, 0)
+        return shape, eps, be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=True)
+
+    def bwd(shape, eps, loc, bstat):
+        saved = dict(y=y, fe_out=fe, fx_out=fx, eps=eps, T=loc["T"], rowstat=loc["rowstat"],
+                     bstat=bstat)
+        flat, _, _ = be.backward_local(shape, saved, gscal, live, g_I, g_IL, 0.1, 200.0, True)
+        return flat
+
+    shape, eps, loc = fwd(S, 0)
+    full = bwd(shape, eps, loc, loc["bstat"])
+    del eps, loc
+    a, b = fwd(1500, 0), fwd(S - 1500, 1500)
+    bstat = be.combine_bstats(torch.stack([a[2]["bstat"], b[2]["bstat"]]))
+    sh = bwd(*a, bstat)
+    sh += bwd(*b, bstat)
+    torch.cuda.synchronize()
+    n = B * L
+    for name, sl in (("d fe_out", slice(0, n)), ("d fx_out", slice(n, 2 * n)),
+                     ("dR", slice(2 * n, None))):
+        assert torch.isfinite(full[sl]).all(), name
+        e = rel_err(_np(sh[sl]), _np(full[sl]))
+        assert e <= 1e-5, (name, e)
 
 
 def test_full_size_train_step_is_finite_and_deterministic():
