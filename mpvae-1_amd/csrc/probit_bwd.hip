@@ -551,6 +551,9 @@ MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0
 #ifndef MPV_MFMA_PHASED
 #define MPV_MFMA_PHASED 0
 #endif
+#ifndef MPV_NOISE16
+#define MPV_NOISE16 0  // study: skip the eps_lo products (timing of f16-exact noise)
+#endif
 template <int TM, int TN>
 MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
   if (MPV_MFMA_PHASED) {  // term by term over all tiles, same order per accumulator
@@ -580,8 +583,9 @@ MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
     for (int n = 0; n < TN; ++n) {
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
                                                          acc[m][n], 0, 0, 0);
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
-                                                         acc[m][n], 0, 0, 0);
+      if (!MPV_NOISE16)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                           acc[m][n], 0, 0, 0);
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
                                                          acc[m][n], 0, 0, 0);
     }

@@ -110,6 +110,9 @@ struct FwdParams {
 #ifndef MPV_FWD_XFER
 #define MPV_FWD_XFER 0  // rebalance the asymmetric forward's epilogue through LDS (study: +1 %)
 #endif
+#ifndef MPV_NOISE16
+#define MPV_NOISE16 0  // study: skip the eps_lo products (timing of f16-exact noise)
+#endif
 #ifndef MPV_FWD_NSTAGE
 #define MPV_FWD_NSTAGE 2  // stage ring depth of the 256 x 128 forward tile
 #endif
@@ -863,8 +866,9 @@ MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
     for (int m = 0; m < TL; ++m)
 #pragma unroll
       for (int n = 0; n < TS; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
-                                                           acc[m][n], 0, 0, 0);
+        if (!MPV_NOISE16)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
+                                                             acc[m][n], 0, 0, 0);
 #pragma unroll
     for (int m = 0; m < TL; ++m)
 #pragma unroll
@@ -1333,7 +1337,7 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
       }
       if (kc < nK) step(f0, f1, false);
     } else {
-      for (int kc = 0; kc < nK; ++kc, ++gs) {
+      for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
         wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
@@ -1344,6 +1348,15 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
         fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
         fwd16t_mfma<TL, TSW>(acc, f);
       }
+    }
+    if (MPV_ABL & 1) {  // timing study: no epilogue
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TSW; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 512 + threadIdx.x] = v;
+      continue;
     }
     if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
     if (X > 0) {
@@ -1383,6 +1396,7 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
         __builtin_amdgcn_s_setprio(0);
     }
   }
+  if (MPV_ABL & 8) wait_vmcnt<0>();  // timing study: no stage DMA left in flight at exit
 }
 
 template <int TSA, int TSB>

@@ -59,7 +59,9 @@ def test_fair_penalty_training_size_against_oracle(norm):
     labels = (rng.random((B, L)) < 0.02).astype(np.int64)
     labels[256:] = labels[:256]
     sens = rng.integers(0, 3, (B, 2)).astype(np.int64)
-    dists = [{"".join(r.astype(str)): float(rng.uniform(0.1, 1)) for r in labels[i::7]}
+    # numpy float64 distances (label_distance*.py's np.clip): the reference's
+    # weights tensor is then float64, and so is the returned loss
+    dists = [{"".join(r.astype(str)): np.float64(rng.uniform(0.1, 1)) for r in labels[i::7]}
              for i in range(3)]
     f = dict(labels=labels, sensitive=sens, dists=dists, norm=norm, coeff=0.5,
              label_z=rng.uniform(0.01, 0.99, (B, L)).astype(np.float32),
@@ -67,6 +69,7 @@ def test_fair_penalty_training_size_against_oracle(norm):
     loss, count, gl, gf = _run(f)
     rl, rc, rgl, rgf = of.fair_penalty(f["label_z"], f["feat_z"], labels, sens, dists, norm, 0.5)
     assert int(count) == rc
+    assert loss.dtype == torch.float64
     assert abs(float(loss) - rl) <= 1e-10 * abs(rl)
     for g, r in ((gl, rgl), (gf, rgf)):
         assert np.abs(g.cpu().numpy() - r).max() <= 1e-6 * np.abs(r).max()

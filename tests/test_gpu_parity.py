@@ -12,7 +12,7 @@ from mpvae_ops import ElboConfig, HipShardBackend, ProbitELBO
 from golden_io import DIFF, OUTS, PART_KEYS, fixtures
 from oracle import philox, probit_elbo as pe
 from tolerances import (EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL,
-                        LONG_K_GRAD_RTOL, rel_err)
+                        HEADLINE_GRAD_RTOL, LONG_K_GRAD_RTOL, rel_err)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -138,7 +138,7 @@ RANDOM_CASES = [
 ]
 
 
-def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed):
+def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True):
     """(forward errors, gradient errors) of the HIP path vs oracle.probit_elbo on
     seeded random inputs with explicit noise."""
     rng = np.random.default_rng(seed)
@@ -151,6 +151,8 @@ def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed):
                r_sqrt_sigma=rng.uniform(-1, 1, (L, z)) * np.sqrt(6.0 / (L + z)))
     noise = f32(rng.standard_normal((S, B, z)))
     g_I, g_IL = f32(rng.standard_normal((B, L))), f32(rng.standard_normal((B, L)))
+    if not with_gI:  # objective = total_loss alone (what bench.py and training backprop)
+        g_I, g_IL = np.zeros_like(g_I), np.zeros_like(g_IL)
     ref = pe.elbo_forward(inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"], inp["fx_out"],
                           inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, nll_coeff,
                           c_coeff)
@@ -184,19 +186,33 @@ def test_random_against_oracle(L, z, B, S, d, gemm):
 
 
 @pytest.mark.parametrize("gemm", ["f16x3", "f32"])
-def test_headline_coefficients_against_oracle(gemm):
+@pytest.mark.parametrize("with_gI", [True, False], ids=["with_gI", "total_only"])
+def test_headline_coefficients_against_oracle(gemm, with_gI):
     """The bench's own coefficients (nll_coeff 0.1, c_coeff 200: main.py:58,62)
     at the headline L = z = 1024 with a realistic batch (B = 64) and small S,
-    against the fp64-reduction oracle at the stated tolerances.  (bench.py's
-    elbo_rel_err compares with the torch-CPU restatement instead, whose fp32
-    1 - E near E -> 1 moves d fe_out by ~2e-3: tests/test_oracle_golden.py
-    pins that spread.)"""
-    ferr, gerr = _against_oracle(1024, 1024, 64, 16, 50, gemm, 0.1, 200.0, 2024)
-    print(gemm, "fwd", ferr, "grad", gerr)
+    against the fp64-reduction oracle.  With upstream gradients on indiv_prob*
+    (fairness / post-processing callers) the stated GRAD_RTOL holds; with
+    total_loss alone the gradients are conditioned at ~1e-4 by the fp32 rounding
+    of t (tolerances.py, HEADLINE_GRAD_RTOL)."""
+    ferr, gerr = _against_oracle(1024, 1024, 64, 16, 50, gemm, 0.1, 200.0, 2024, with_gI=with_gI)
+    print(gemm, with_gI, "fwd", ferr, "grad", gerr)
+    for k, e in ferr.items():
+        assert e <= FWD_RTOL, (k, e)
+    gtol = GRAD_RTOL if with_gI else HEADLINE_GRAD_RTOL
+    for k, e in gerr.items():
+        assert e <= gtol, (k, e)
+
+
+def test_headline_batch_against_oracle():
+    """bench.py's parity slice: B = 512, L = z = 1024, S = 2 at the headline
+    coefficients, total_loss as the objective (tolerances.py,
+    HEADLINE_GRAD_RTOL: conditioned at ~1e-4 by the fp32 rounding of t)."""
+    ferr, gerr = _against_oracle(1024, 1024, 512, 2, 50, "f16x3", 0.1, 200.0, 77, with_gI=False)
+    print("fwd", ferr, "grad", gerr)
     for k, e in ferr.items():
         assert e <= FWD_RTOL, (k, e)
     for k, e in gerr.items():
-        assert e <= GRAD_RTOL, (k, e)
+        assert e <= HEADLINE_GRAD_RTOL, (k, e)
 
 
 def test_shard_invariance_at_c4_size():

@@ -146,8 +146,8 @@ def test_torch_port_spread_at_headline_coefficients():
     elements with E -> 1 (u ~ 4.9, 1 - E ~ 1e-6): there one fp32 ulp of E
     (6e-8, from t's fp32 sgemm rounding) is ~6 % of 1 - E, and d log(1 - E)
     = -1/(1 - E) carries it into the gradient.  The GPU is held to the oracle
-    at GRAD_RTOL on the same kind of slice (test_gpu_parity.py::
-    test_headline_coefficients_against_oracle)."""
+    at HEADLINE_GRAD_RTOL (half this spread) on such slices
+    (test_gpu_parity.py::test_headline_*)."""
     import torch
     from oracle import torch_ref
     B, L, z, S, d = 64, 1024, 1024, 1, 50

@@ -24,6 +24,18 @@ GRAD_RTOL = 5e-5
 # 6.1e-5 on the test_random_against_oracle case (4096, 4096, 1, 40) --
 # measured, DESIGN.md section 4.  Allowed: 5x that spread.
 LONG_K_GRAD_RTOL = 5e-4
+# The headline coefficients (nll_coeff 0.1, c_coeff 200, L = z = 1024) with
+# total_loss as the objective: the fp32 rounding of t = eps . R^T alone moves
+# the gradients at the 1e-4 level (the oracle with t from an fp32 sgemm, as
+# the reference's tensordot computes it, instead of fp64: d fx_out 2.6e-4,
+# d fe_out 1.6e-4 on bench.py's B = 512, S = 2 slice; 8e-6 at B = 64, S = 16),
+# and the reference restated in torch-CPU sits 1.9e-3 (d fe_out) / 3.9e-4 (dR)
+# from the oracle (tests/test_oracle_golden.py pins it: its fp32 1 - E near
+# E -> 1).  Stated: 1e-3, i.e. at least as close to the oracle as the reference
+# itself.  Measured on the GPU: <= 1.4e-4 (f16x3; reproduced to 3 digits by a
+# numpy emulation of its arithmetic: 3xf16 products added to the fp32
+# accumulator term by term), <= 3e-5 (exact-fp32 MFMA mode).
+HEADLINE_GRAD_RTOL = 1e-3
 EXTREME_FWD_RTOL = 1e-3
 EXTREME_GRAD_RTOL = 5e-2
 
