@@ -89,6 +89,9 @@ def step(y, leaves, args, it):
     for v in leaves.values():
         v.grad = None
     args.mpvae_seed = 0x5EED0000 + it
+    if args.mode != "train":  # evaluation: forward only, no autograd state
+        with torch.no_grad():
+            return mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
     out = mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
     out[0].backward()
     return out
@@ -215,6 +218,11 @@ def main():
     ap.add_argument("--cpu-sample-s", type=int, default=2)
     ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--gemm", default="f16x3", choices=sorted(PEAKS))
+    # eval: the forward-only evaluation call (fairsoft_evaluate.py:40,72-74 with
+    # fairsoft_trial.py:70: mode 'test', n_sample = n_test_sample = 10000 unless
+    # --eval-samples); not the headline metric
+    ap.add_argument("--mode", default="train", choices=["train", "eval"])
+    ap.add_argument("--eval-samples", type=int, default=10000)
     cli = ap.parse_args()
 
     world, rank, local = setup_dist()
@@ -223,10 +231,13 @@ def main():
         log(f"warning: --gpus {cli.gpus} but WORLD_SIZE {world}; using {world}")
     device = torch.device("cuda", local)
     L, z, B, S, d, nllc, cc, scaling = CONFIGS[cli.config]
+    if cli.mode == "eval":
+        S = cli.eval_samples
     S_total = S * world if scaling == "weak" else S
     S_local = S if scaling == "weak" else S // world
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_total,
-                              n_test_sample=S_total, mode="train", nll_coeff=nllc, c_coeff=cc,
+                              n_test_sample=S_total, mode="train" if cli.mode == "train" else "test",
+                              nll_coeff=nllc, c_coeff=cc,
                               mpvae_noise="philox", mpvae_shard=world > 1 or forced,
                               mpvae_force_exchange=forced, mpvae_gemm=cli.gemm)
     y, leaves = make_inputs(L, z, B, d, device)
@@ -256,11 +267,12 @@ def main():
     finite = bool(torch.isfinite(out[0]).item())
     value = S_total * B * L * cli.steps / elapsed
     rl = roofline(times, S_local, B, L, z, cli.steps, cli.gemm)
-    rl["traffic"], rl["traffic_source"] = pmc_traffic(cli.config, rl["kernel"])
-    rl["rocprof_avg_ms"] = trace_avg_ms(cli.config, rl["kernel"])
+    prof_key = cli.config if cli.mode == "train" else cli.config + "eval"
+    rl["traffic"], rl["traffic_source"] = pmc_traffic(prof_key, rl["kernel"])
+    rl["rocprof_avg_ms"] = trace_avg_ms(prof_key, rl["kernel"])
 
     cpu, errs = None, None
-    if rank == 0 and world == 1 and not cli.no_cpu_baseline:
+    if rank == 0 and world == 1 and not cli.no_cpu_baseline and cli.mode == "train":
         S_cpu = max(1, min(cli.cpu_sample_s, S))
         cpu, errs = cpu_baseline(L, z, B, d, S_cpu, cli.cpu_reps, device)
 
@@ -270,7 +282,9 @@ def main():
             "steps": cli.steps, "warmup": cli.warmup, "ms_per_step": elapsed / cli.steps * 1e3,
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"{cli.config}: compute_loss fwd+bwd, B={B}, L={L}, z={z}, "
+            "config": {"workload": f"{cli.config}: compute_loss "
+                                   f"{'fwd+bwd' if cli.mode == 'train' else 'forward only (eval)'}, "
+                                   f"B={B}, L={L}, z={z}, "
                                    f"n_sample={S_total} ({S_local}/GPU), philox noise on device",
                        "global_batch": B, "n_sample": S_total, "label_dim": L, "z_dim": z,
                        "parallelism": f"n_sample-sharded x{world}", "gemm": cli.gemm},

@@ -189,10 +189,13 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
 // ONE: a block row covers all its columns (RPI == 1), so the row index and the
 // six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
 #ifndef MPV_ELEM_LA
-#define MPV_ELEM_LA 3
+#define MPV_ELEM_LA 1
+#endif
+#ifndef MPV_ELEM_WPS
+#define MPV_ELEM_WPS 4  // minimum waves per SIMD the element pass is compiled for (128 VGPRs)
 #endif
 template <bool VEC, bool PLANES, bool ONE>
-__global__ __launch_bounds__(256) void bwd_elem_kernel(ElemParams p) {
+__global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams p) {
   constexpr int LA = MPV_ELEM_LA;
   __shared__ float cred[256 * 8];
   const int b = blockIdx.x, sc = blockIdx.y;
