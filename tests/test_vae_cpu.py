@@ -61,3 +61,41 @@ def test_checkpoint_round_trip(tmp_path):
     b.load_state_dict(torch.load(p, weights_only=True))
     for (ka, va), (kb, vb) in zip(a.state_dict().items(), b.state_dict().items()):
         assert ka == kb and torch.equal(va, vb)
+
+
+def test_batched_step_syncs_match_the_reference_semantics():
+    """mpvae_step: has_finite_grad gives the reference's
+    per-parameter answer (fairsoft_utils.py:28-41) with one sync, step_scalars
+    the .item() values with one copy."""
+    import mpvae_step as ms
+
+    def ref_has_finite_grad(model):  # fairsoft_utils.py:28-41, restated
+        if isinstance(model, torch.Tensor):
+            return not (torch.isnan(model.grad).any() or torch.isinf(model.grad).any())
+        ok = True
+        for p in model.parameters():
+            if p.grad is not None:
+                ok = ok and not (torch.isnan(p.grad).any() or torch.isinf(p.grad).any())
+        return ok
+
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = mpvae.VAE(_args())
+    assert ms.has_finite_grad(model) is True  # no gradients yet
+    for p in model.parameters():
+        p.grad = torch.randn_like(p)
+    assert ms.has_finite_grad(model) == ref_has_finite_grad(model) is True
+    for bad in (float("nan"), float("inf"), -float("inf")):
+        model.fd2.weight.grad[1, 2] = bad
+        assert ms.has_finite_grad(model) == ref_has_finite_grad(model) is False
+        model.fd2.weight.grad[1, 2] = 0.0
+    model.r_sqrt_sigma.grad = None
+    assert ms.has_finite_grad(model) is True
+    t = torch.zeros(3, requires_grad=True)
+    t.grad = torch.tensor([1.0, float("nan"), 0.0])
+    assert ms.has_finite_grad(t) is False
+    vals = dict(total_loss=torch.tensor(1.5), nll_loss=torch.tensor(0.25, dtype=torch.float64),
+                macro_f1=torch.tensor([0.75]).reshape(()), success_updates=3)
+    got = ms.step_scalars(**vals)
+    assert got == {"total_loss": 1.5, "nll_loss": 0.25, "macro_f1": 0.75, "success_updates": 3}
+    assert all(type(got[k]) is float for k in ("total_loss", "nll_loss", "macro_f1"))

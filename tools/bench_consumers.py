@@ -70,6 +70,38 @@ def main():
         lib.mpv_timing_enable(0)
         kt = {k: round(v[1] / cli.reps, 4) for k, v in H.kernel_times().items()}
         res[name] = {"wall_ms": round(wall, 4), "kernel_ms": kt}
+    # per-step host syncs after backward (fairsoft_train.py:141-162): the
+    # reference's has_finite_grad (two host bools per parameter) and eight
+    # .item() calls, against mpvae_step's one reduction + one copy each
+    import argparse as _ap
+    import mpvae
+    import mpvae_step as ms
+    vargs = _ap.Namespace(feature_dim=1000, latent_dim=50, label_dim=L, z_dim=L, keep_prob=0.5,
+                          scale_coeff=1.0, residue_sigma="")
+    model = mpvae.VAE(vargs).to(dev)
+    for prm in model.parameters():
+        prm.grad = torch.randn_like(prm)
+    scal = {f"s{i}": torch.rand((), device=dev) for i in range(8)}
+
+    def ref_syncs():
+        ok = True
+        for prm in model.parameters():
+            if prm.grad is not None:
+                ok = ok and not (torch.isnan(prm.grad).any() or torch.isinf(prm.grad).any())
+        return ok, [v.item() for v in scal.values()]
+
+    def batched_syncs():
+        return ms.has_finite_grad(model), ms.step_scalars(**scal)
+
+    for name, fn in (("step_syncs_reference", ref_syncs), ("step_syncs_batched", batched_syncs)):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(cli.reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name + "_ms"] = round((time.perf_counter() - t0) / cli.reps * 1e3, 4)
     t0 = time.perf_counter()
     of.fair_penalty(lz_np, fz_np, labels, sens, dists, "l1", 0.5)
     res["fairness_cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
