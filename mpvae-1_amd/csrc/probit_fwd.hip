@@ -890,6 +890,45 @@ MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
     }
 }
 
+// Packed fp32 fma with the scalar operands broadcast from one half of a
+// register pair by op_sel.  hipcc does not fold such splats of a VGPR element
+// (a per-lane label constant) into op_sel: it materialises each splat with
+// two v_mov per use, ~10 % of the epilogue's VALU instructions.
+#ifndef MPV_EPI_BC
+#define MPV_EPI_BC 1
+#endif
+// a * b[H] + c[H]
+template <int H>
+MPV_DEV f32x2 pk_fma_bc(f32x2 a, f32x2 b, f32x2 c) {
+  if (!MPV_EPI_BC) return pk_fma(a, splat2(b[H]), splat2(c[H]));
+  f32x2 d;
+  if (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[1,1,1]"
+        : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// sp += p[H] * r, sn += q[H] * r, with r fresh from v_exp_f32 (the s_nop is
+// the wait state a VALU read of a transcendental's result needs on gfx950,
+// which hipcc does not insert for an asm statement's inputs)
+template <int H>
+MPV_DEV void pk_fma2_acc_bc(f32x2 p, f32x2 q, f32x2 r, f32x2& sp, f32x2& sn) {
+  if (MPV_EPI_BC != 1) {  // 2: only pk_fma_bc in asm
+    sp = pk_fma(splat2(p[H]), r, sp);
+    sn = pk_fma(splat2(q[H]), r, sn);
+    return;
+  }
+  if (H == 0)
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %2, %4, %0 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %1, %3, %4, %1 op_sel_hi:[0,1,1]"
+        : "+v"(sp), "+v"(sn) : "v"(p), "v"(q), "v"(r));
+  else
+    asm("s_nop 0\n\tv_pk_fma_f32 %0, %2, %4, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %1, %3, %4, %1 op_sel:[1,0,0] op_sel_hi:[1,1,1]"
+        : "+v"(sp), "+v"(sn) : "v"(p), "v"(q), "v"(r));
+}
+
 // acc[m][n][i] = t of sample (ws*TS+n)*16 + lr, label (wl*TL+m)*16 + 4*lg + i.
 // Masks are carried as 0/1 float weights (VGPRs) rather than lane masks: the
 // 16 per-label masks of a label group would otherwise pin ~40 SGPRs and spill.
@@ -1010,6 +1049,13 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const f32x4 sgb = *reinterpret_cast<const f32x4*>(cols + kCsgb * BN + lb);
     const f32x4 wpos = *reinterpret_cast<const f32x4*>(cols + kCwpos * BN + lb);
     const f32x4 wneg = *reinterpret_cast<const f32x4*>(cols + kCwneg * BN + lb);
+    // the same constants as register pairs (labels 0,1 | 2,3) for pk_fma_bc
+    const f32x2 qa2[2] = {f32x2{qa[0], qa[1]}, f32x2{qa[2], qa[3]}};
+    const f32x2 qb2[2] = {f32x2{qb[0], qb[1]}, f32x2{qb[2], qb[3]}};
+    const f32x2 sga2[2] = {f32x2{sga[0], sga[1]}, f32x2{sga[2], sga[3]}};
+    const f32x2 sgb2[2] = {f32x2{sgb[0], sgb[1]}, f32x2{sgb[2], sgb[3]}};
+    const f32x2 wpos2[2] = {f32x2{wpos[0], wpos[1]}, f32x2{wpos[2], wpos[3]}};
+    const f32x2 wneg2[2] = {f32x2{wneg[0], wneg[1]}, f32x2{wneg[2], wneg[3]}};
     f32x2 ce[4] = {splat2(0.0f), splat2(0.0f), splat2(0.0f), splat2(0.0f)};
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
@@ -1029,9 +1075,11 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // BCE operand (mpvae.py:184-185): E for y = 1, 1 - E for y = 0, 1 for a pad label
-        q[i] = pk_fma(w4[i], splat2(qa[i]), splat2(qb[i]));
+        q[i] = (i & 1) ? pk_fma_bc<1>(w4[i], qa2[i >> 1], qb2[i >> 1])
+                       : pk_fma_bc<0>(w4[i], qa2[i >> 1], qb2[i >> 1]);
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-        const f32x2 a = pk_fma(w4[i], splat2(sga[i]), splat2(sgb[i]));
+        const f32x2 a = (i & 1) ? pk_fma_bc<1>(w4[i], sga2[i >> 1], sgb2[i >> 1])
+                                : pk_fma_bc<0>(w4[i], sga2[i >> 1], sgb2[i >> 1]);
         r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       }
       // sum of the 4 labels' log-probs as ONE log of their product (log2 units,
@@ -1054,8 +1102,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       sl[n] = sl[n] + lp;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        sp[n] = pk_fma(splat2(wpos[i]), r[i], sp[n]);
-        sn[n] = pk_fma(splat2(wneg[i]), r[i], sn[n]);
+        if (i & 1)
+          pk_fma2_acc_bc<1>(wpos2[i >> 1], wneg2[i >> 1], r[i], sp[n], sn[n]);
+        else
+          pk_fma2_acc_bc<0>(wpos2[i >> 1], wneg2[i >> 1], r[i], sp[n], sn[n]);
         ce[i] = pk_fma(splat2(wr), w4[i], ce[i]);  // sum E = kEh sum w + C0 count
       }
       // MPV_EPI_SB samples at a time: bounded live ranges vs more independent chains
