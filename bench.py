@@ -97,6 +97,48 @@ def step(y, leaves, args, it):
     return out
 
 
+def graph_steps(y, leaves, args, warmup, steps):
+    """Capture one fwd+bwd step in a HIP graph and time `steps` replays.  The
+    Philox key is a device tensor advanced inside the graph, so every replay
+    draws fresh noise (tests/test_gpu_parity.py checks replays against eager)."""
+    seed = torch.tensor([0x5EED0000], dtype=torch.int64, device=y.device)
+    args.mpvae_seed = seed
+    # fresh leaves: their AccumulateGrad nodes are created on the capture's
+    # side stream, not on the default stream of the eager pass
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in leaves.items()}
+
+    def one():
+        for v in leaves.values():
+            v.grad = None
+        seed.add_(1)
+        if args.mode != "train":
+            with torch.no_grad():
+                return mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
+        out = mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
+        out[0].backward()
+        return out
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(max(2, warmup)):
+            one()
+    torch.cuda.current_stream().wait_stream(side)
+    for v in leaves.values():
+        v.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = one()
+    for _ in range(max(1, warmup)):
+        graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    return out, time.perf_counter() - t0
+
+
 def roofline(times, S_local, B, L, z, steps, gemm):
     """Dominant kernel's achieved rate vs its bound, from in-library HIP events.
     GEMM work is the algorithmic fp32 GEMM (2*S*B*L*z flops per launch)."""
@@ -223,6 +265,10 @@ def main():
     # --eval-samples); not the headline metric
     ap.add_argument("--mode", default="train", choices=["train", "eval"])
     ap.add_argument("--eval-samples", type=int, default=10000)
+    # graph: the step captured once in a HIP graph (torch.cuda.graph) and replayed,
+    # its Philox key a device tensor the step advances (mpv_noise_philox*_dev);
+    # per-kernel times (roofline) come from an eager pass of the same step
+    ap.add_argument("--graph", action="store_true")
     cli = ap.parse_args()
 
     world, rank, local = setup_dist()
@@ -260,6 +306,14 @@ def main():
     elapsed = time.perf_counter() - t0
     lib.mpv_timing_enable(0)
     times = H.kernel_times()
+    graph_note = None
+    if cli.graph:
+        if world > 1 or forced:
+            raise SystemExit("--graph runs one process (no collectives in the captured step)")
+        del out  # the eager pass's autograd graph
+        out, elapsed = graph_steps(y, leaves, args, cli.warmup, cli.steps)
+        graph_note = "HIP graph replay of the captured step (ms_per_step, value); roofline " \
+                     "kernel times from the eager pass of the same step"
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -290,6 +344,8 @@ def main():
                        "parallelism": f"n_sample-sharded x{world}", "gemm": cli.gemm},
             "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
         }
+        if graph_note:
+            line["graph"] = graph_note
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 3
+#define MPV_ABI_VERSION 4  /* 4: device-memory Philox keys (mpv_noise_philox*_dev) */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -59,6 +59,14 @@ const char* mpv_last_error(void);
  * ((s_offset+s)*B+b)*z+k, so any S-sharding draws the same noise. */
 int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t offset,
                      void* stream);
+
+/* The same draw with the 64-bit Philox key read from device memory at run
+ * time (seed_dev: one uint64 in device memory), so a step captured in a HIP
+ * graph draws fresh noise on each replay when the step advances that word,
+ * and the sharded path agrees on rank 0's key by a broadcast with no host
+ * sync.  Same numbers as mpv_noise_philox with seed = *seed_dev. */
+int mpv_noise_philox_dev(float* eps, const mpv_shape* shape, const uint64_t* seed_dev,
+                         uint64_t offset, void* stream);
 
 /* Raw Philox4x32-10 words (known-answer tests): out[4*i..4*i+3] =
  * philox(counter = ctr0 + i (as lo,hi,0,0), key = key). */
@@ -97,6 +105,11 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
  * GEMMs stream them); the same numbers as mpv_noise_philox. */
 int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
                          const mpv_split16* out, void* stream);
+
+/* mpv_noise_philox_f16 with the key read from device memory (see
+ * mpv_noise_philox_dev). */
+int mpv_noise_philox_f16_dev(const mpv_shape* shape, const uint64_t* seed_dev, uint64_t offset,
+                             const mpv_split16* out, void* stream);
 
 /* Element-wise dtype conversion; replaces r_sqrt_sigma.T.float() (mpvae.py:165)
  * and the fp32 -> fp64 cast of its gradient in autograd. */

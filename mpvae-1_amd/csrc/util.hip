@@ -84,8 +84,21 @@ int check_shape(const mpv_shape* s) {
 
 // ------------------------------------------------------------- Philox noise
 // One thread = one Philox counter = 4 consecutive noise elements.
+// The Philox key: the host value, or (seed_dev != nullptr) the 64-bit word
+// at seed_dev, read on the device at run time -- so a captured graph draws
+// fresh noise each replay when the step bumps that word.
+MPV_DEV void philox_key(const uint64_t* seed_dev, uint32_t& k0, uint32_t& k1) {
+  if (seed_dev != nullptr) {
+    const uint64_t k = __builtin_nontemporal_load(seed_dev);
+    k0 = (uint32_t)k;
+    k1 = (uint32_t)(k >> 32);
+  }
+}
+
 __global__ void noise_philox_kernel(float* __restrict__ eps, int64_t e_begin, int64_t e_count,
-                                    uint32_t k0, uint32_t k1, uint64_t offset) {
+                                    uint32_t k0, uint32_t k1, uint64_t offset,
+                                    const uint64_t* __restrict__ seed_dev) {
+  philox_key(seed_dev, k0, k1);
   const int64_t g0 = e_begin >> 2;  // first counter touching the shard
   const int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t e_end = e_begin + e_count;
@@ -274,7 +287,9 @@ constexpr float kNoiseScale = 4096.0f;
 __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
                                                             int z, int64_t s_off, uint32_t k0,
                                                             uint32_t k1, uint64_t offset,
-                                                            int rows) {
+                                                            int rows,
+                                                            const uint64_t* __restrict__ seed_dev) {
+  philox_key(seed_dev, k0, k1);
   const int r_end = min(rows, (int)(blockIdx.x + 1) * MPV_NOISE_ROWS);
   for (int r = blockIdx.x * MPV_NOISE_ROWS; r < r_end; ++r) {
   const int bb = r / S, ss = r - bb * S;
@@ -370,8 +385,8 @@ int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms) {
 
 const char* mpv_last_error(void) { return g_err; }
 
-int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t offset,
-                     void* stream) {
+static int noise_philox(float* eps, const mpv_shape* shape, uint64_t seed,
+                        const uint64_t* seed_dev, uint64_t offset, void* stream) {
   if (int rc = check_shape(shape)) return rc;
   MPV_REQUIRE(eps != nullptr, "eps is NULL");
   const int64_t per_s = shape->B * shape->z;
@@ -384,8 +399,19 @@ int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t
   MPV_REQUIRE(blocks < (int64_t(1) << 31), "noise too large");
   MPV_LAUNCH("noise_philox", noise_philox_kernel, dim3((unsigned)blocks), dim3(threads), 0,
                      as_stream(stream), eps, e_begin, e_count, (uint32_t)seed,
-                     (uint32_t)(seed >> 32), offset);
+                     (uint32_t)(seed >> 32), offset, seed_dev);
   return check_launch("noise_philox");
+}
+
+int mpv_noise_philox(float* eps, const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                     void* stream) {
+  return noise_philox(eps, shape, seed, nullptr, offset, stream);
+}
+
+int mpv_noise_philox_dev(float* eps, const mpv_shape* shape, const uint64_t* seed_dev,
+                         uint64_t offset, void* stream) {
+  MPV_REQUIRE(seed_dev != nullptr, "seed_dev is NULL");
+  return noise_philox(eps, shape, 0, seed_dev, offset, stream);
 }
 
 int mpv_philox_raw(uint32_t* out, int64_t n, uint64_t ctr0, uint64_t key, void* stream) {
@@ -429,8 +455,8 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
   return check_launch("split_f16");
 }
 
-int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
-                         const mpv_split16* out, void* stream) {
+static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_t* seed_dev,
+                            uint64_t offset, const mpv_split16* out, void* stream) {
   if (int rc = check_shape(shape)) return rc;
   if (int rc = check_split(out)) return rc;
   const int64_t rows = shape->S_local * shape->B;
@@ -441,8 +467,19 @@ int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
   const unsigned threads = out->ld / 8 >= 256 ? 256 : (unsigned)(cdiv(out->ld / 8, 64) * 64);
   MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(rows, MPV_NOISE_ROWS)),
              dim3(threads), 0, s, *out, (int)shape->S_local, (int)shape->B, (int)shape->z,
-             shape->s_offset, (uint32_t)seed, (uint32_t)(seed >> 32), offset, (int)rows);
+             shape->s_offset, (uint32_t)seed, (uint32_t)(seed >> 32), offset, (int)rows, seed_dev);
   return check_launch("noise_philox_f16");
+}
+
+int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
+                         const mpv_split16* out, void* stream) {
+  return noise_philox_f16(shape, seed, nullptr, offset, out, stream);
+}
+
+int mpv_noise_philox_f16_dev(const mpv_shape* shape, const uint64_t* seed_dev, uint64_t offset,
+                             const mpv_split16* out, void* stream) {
+  MPV_REQUIRE(seed_dev != nullptr, "seed_dev is NULL");
+  return noise_philox_f16(shape, 0, seed_dev, offset, out, stream);
 }
 
 int mpv_convert(const void* src, int sd, void* dst, int dd, int64_t n, void* stream) {

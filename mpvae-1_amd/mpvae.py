@@ -154,6 +154,9 @@ def _noise_source(args, n_sample, B, z, shard, device):
         noise = torch.normal(0, 1, size=(n_sample, B, z))
         return noise[s0:s1].to(device), dict(noise="explicit")
     if mode == "philox":
+        # args.mpvae_seed: an int, or a one-element int64 tensor on the device
+        # whose value the noise kernel reads at run time (no host sync; a step
+        # captured in a HIP graph draws fresh noise when the tensor advances)
         seed = getattr(args, "mpvae_seed", None)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())

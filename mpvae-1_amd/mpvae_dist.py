@@ -70,7 +70,13 @@ class SampleShardExchange:
         return 0 if self.group is None else dist.get_global_rank(self.group, 0)
 
     def agree_seed(self, seed, device):
-        """The Philox seed of the group's rank 0, on every rank."""
+        """The Philox seed of the group's rank 0, on every rank.  A device
+        tensor seed is broadcast into a copy and stays on the device (no host
+        sync); an int comes back as an int."""
+        if isinstance(seed, torch.Tensor):
+            t = seed.detach().to(device=device, dtype=torch.int64).reshape(1).clone()
+            dist.broadcast(t, src=self._src(), group=self.group)
+            return t
         u = int(seed) & (2 ** 64 - 1)  # the 64-bit Philox key, carried as int64
         t = torch.tensor([u - 2 ** 64 if u >= 2 ** 63 else u], dtype=torch.int64, device=device)
         dist.broadcast(t, src=self._src(), group=self.group)

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -110,6 +110,9 @@ SIGNATURES = {
                                      ctypes.POINTER(Split16), vp, vp]),
     "mpv_noise_philox_f16": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.c_uint64,
                                             ctypes.c_uint64, ctypes.POINTER(Split16), vp]),
+    "mpv_noise_philox_dev": (ctypes.c_int, [vp, ctypes.POINTER(Shape), vp, ctypes.c_uint64, vp]),
+    "mpv_noise_philox_f16_dev": (ctypes.c_int, [ctypes.POINTER(Shape), vp, ctypes.c_uint64,
+                                                ctypes.POINTER(Split16), vp]),
     "mpv_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
     "mpv_probit_fwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FwdArgs), vp]),
     "mpv_bstat_combine": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int64, vp, vp]),

@@ -72,14 +72,30 @@ class HipShardBackend:
         return H.Shape(S_local, S_total, s_offset, B, L, z)
 
     def make_noise(self, shape, device, seed, offset):
+        """Philox noise for this shard.  seed: an int (the key, passed by value)
+        or a one-element int64 device tensor holding it (read by the kernel at
+        run time: graph-capturable, no host sync)."""
         lib, st = H.load_library(), H.stream_of(device)
+        dev_key = isinstance(seed, torch.Tensor)
+        if dev_key and (seed.dtype != torch.int64 or seed.numel() != 1 or
+                        seed.device != torch.device(device)):
+            raise ValueError("a device Philox seed must be a one-element int64 tensor on "
+                             f"{device} (got {seed.dtype}, {seed.numel()} elements, {seed.device})")
         if self.gemm == H.GEMM_F16X3:
             eps = Planes(shape.S_local * shape.B, _pad(shape.z, EPS_PAD), device)
-            H.check(lib.mpv_noise_philox_f16(shape, seed, offset, eps.c(), st),
-                    "mpv_noise_philox_f16")
+            if dev_key:
+                H.check(lib.mpv_noise_philox_f16_dev(shape, H.ptr(seed), offset, eps.c(), st),
+                        "mpv_noise_philox_f16_dev")
+            else:
+                H.check(lib.mpv_noise_philox_f16(shape, seed, offset, eps.c(), st),
+                        "mpv_noise_philox_f16")
             return eps
         eps = torch.empty((shape.S_local, shape.B, shape.z), device=device, dtype=torch.float32)
-        H.check(lib.mpv_noise_philox(H.ptr(eps), shape, seed, offset, st), "mpv_noise_philox")
+        if dev_key:
+            H.check(lib.mpv_noise_philox_dev(H.ptr(eps), shape, H.ptr(seed), offset, st),
+                    "mpv_noise_philox_dev")
+        else:
+            H.check(lib.mpv_noise_philox(H.ptr(eps), shape, seed, offset, st), "mpv_noise_philox")
         return eps
 
     def _split(self, x, rows, cols, planes):
@@ -218,7 +234,9 @@ class ElboConfig:
                  seed=0, offset=0, backend=None, exchange=None, gemm="f16x3"):
         self.S_total, self.S_local, self.s_offset = int(S_total), int(S_local), int(s_offset)
         self.nll_coeff, self.c_coeff = float(nll_coeff), float(c_coeff)
-        self.noise, self.seed, self.offset = noise, int(seed), int(offset)
+        # seed: an int, or a one-element int64 device tensor (HipShardBackend.make_noise)
+        self.noise, self.offset = noise, int(offset)
+        self.seed = seed if isinstance(seed, torch.Tensor) else int(seed)
         self.backend = backend if backend is not None else HipShardBackend(gemm)
         self.exchange = exchange if exchange is not None else LocalExchange()
 

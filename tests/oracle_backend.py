@@ -26,6 +26,8 @@ class OracleShardBackend:
 
     def make_noise(self, shape, device, seed, offset):
         from oracle import philox
+        if isinstance(seed, torch.Tensor):  # a device-memory key (mpv_noise_philox*_dev)
+            seed = int(seed.reshape(-1)[0]) & (2 ** 64 - 1)
         return _t(philox.normal_noise(shape.S_local, shape.B, shape.z, seed, offset,
                                       shape.s_offset))
 

@@ -91,7 +91,9 @@ def _replica_worker(rank, world, port, q):
         from oracle_backend import OracleShardBackend
         f = next(f for f in fixtures() if f.name == "f1_l38")
         ex = SampleShardExchange(verify=True)
-        seeds = (ex.agree_seed(1000 + rank, "cpu"), ex.agree_seed(2 ** 64 - 1 - rank, "cpu"))
+        dev_seed = ex.agree_seed(torch.tensor([7000 + rank], dtype=torch.int64), "cpu")
+        seeds = (ex.agree_seed(1000 + rank, "cpu"), ex.agree_seed(2 ** 64 - 1 - rank, "cpu"),
+                 int(dev_seed[0]), tuple(dev_seed.shape), str(dev_seed.dtype))
         S_local, s_off = split_samples(f.S, world, rank)
         t = {k: torch.from_numpy(f[k].copy()) for k in
              ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar",
@@ -128,5 +130,5 @@ def test_replica_contract_is_enforced():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, seeds, outcome in results:
-        assert seeds == (1000, 2 ** 64 - 1), (rank, seeds)
+        assert seeds == (1000, 2 ** 64 - 1, 7000, (1,), "torch.int64"), (rank, seeds)
         assert outcome == ["ok", "mismatch"], (rank, outcome)

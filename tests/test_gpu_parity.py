@@ -108,6 +108,79 @@ def test_philox_noise_matches_oracle(S, B, z, s_off):
     assert not v[:, z:].any()
 
 
+@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
+def test_device_seed_noise_is_the_host_seed_noise(gemm):
+    """mpv_noise_philox*_dev (key read from device memory) draws exactly what
+    the by-value entry points draw for the same key."""
+    be = HipShardBackend(gemm)
+    shape = H.Shape(37, 37 + 11, 11, 5, 4, 40)
+    for key in (0x1234ABCD5678, 2 ** 64 - 3):
+        a = be.make_noise(shape, DEV, key, 0)
+        dkey = torch.tensor([key - 2 ** 64 if key >= 2 ** 63 else key], dtype=torch.int64,
+                            device=DEV)
+        b = be.make_noise(shape, DEV, dkey, 0)
+        if gemm == "f16x3":
+            assert torch.equal(a.data, b.data) and torch.equal(a.scale, b.scale)
+        else:
+            assert torch.equal(a, b)
+    with pytest.raises(ValueError):
+        be.make_noise(shape, DEV, torch.tensor([1], dtype=torch.int32, device=DEV), 0)
+
+
+def test_graph_captured_step_draws_fresh_noise_per_replay():
+    """A compute_loss fwd+bwd captured in a HIP graph (torch.cuda.graph) with a
+    device-tensor Philox seed that the step advances: every replay equals an
+    eager step with that seed, bit for bit, and replays draw different noise."""
+    B, L, z, d, S = 16, 38, 38, 8, 64
+    g = torch.Generator(device=DEV).manual_seed(8)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.3).float()
+    y[:, 0], y[:, 1] = 1, 0
+    mk = lambda *sh: torch.randn(*sh, device=DEV, generator=g)
+    base = [mk(B, L), mk(B, d), 0.1 * mk(B, d), mk(B, L), mk(B, d), 0.1 * mk(B, d),
+            (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.2]
+    leaves = [x.clone().requires_grad_(True) for x in base]
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    mk_args = lambda sd: argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S,
+                                            n_test_sample=S, mode="train", nll_coeff=0.5,
+                                            c_coeff=10.0, mpvae_noise="philox", mpvae_seed=sd)
+    args = mk_args(seed)
+
+    def step():
+        seed.add_(1)
+        out = mpvae.compute_loss(y, *leaves, args)
+        out[0].backward()
+        return out
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            for v in leaves:
+                v.grad = None
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    for v in leaves:
+        v.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = step()
+    got = []
+    for _ in range(3):
+        used = int(seed.item()) + 1
+        graph.replay()
+        torch.cuda.synchronize()
+        got.append((used, [o.detach().clone() for o in out], [v.grad.clone() for v in leaves]))
+    assert not torch.equal(got[0][1][0], got[1][1][0])
+    for used, outs, grads in got:
+        ref_leaves = [x.clone().requires_grad_(True) for x in base]
+        ref = mpvae.compute_loss(y, *ref_leaves, mk_args(used))
+        ref[0].backward()
+        for a, b in zip(outs, ref):
+            assert torch.equal(a, b.detach())
+        for a, v in zip(grads, ref_leaves):
+            assert torch.equal(a, v.grad)
+
+
 def test_split_planes_round_trip():
     """mpv_split_f16: power-of-two scale from max|x|, hi+lo == x to ~2^-22."""
     be = HipShardBackend("f16x3")
