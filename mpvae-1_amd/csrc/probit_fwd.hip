@@ -126,7 +126,7 @@ struct FwdParams {
 #define MPV_MFMA_PHASED 1  // term-by-term MFMA issue (same per-accumulator order): -0.75 %
 #endif
 #ifndef MPV_EPI_SB
-#define MPV_EPI_SB 4
+#define MPV_EPI_SB 5
 #endif
 #ifndef MPV_FWD_STAG_MODE
 #define MPV_FWD_STAG_MODE 0
