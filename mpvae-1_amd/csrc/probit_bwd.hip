@@ -383,23 +383,33 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
   }
 }
 
-// One stage's LDS-DMA for this wave: PER_WAVE 1-KB pieces (whole rows).
+// One stage's LDS-DMA for this wave: PER_WAVE 1-KB pieces of RPP whole rows.
 // Wave w moves pieces w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E.
-template <int PER_WAVE, int PIECES>
+// The global base address is the piece's first row (wave-uniform: it goes in
+// an SGPR pair); with RPP > 1 a lane's row within the piece is in its offset.
+template <int PER_WAVE, int PIECES, int RPP>
 MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
-                      const int (&dma_r)[PER_WAVE], const int (&dma_off)[PER_WAVE]) {
+                      const int (&dma_off)[PER_WAVE]) {
+  const int lrow = RPP == 1 ? 0 : (int)(threadIdx.x & 63) / (64 / RPP);
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int pc = wid * PER_WAVE + i;
-    const int q = q0 + dma_r[i];
-    const uint16_t* src = pc < PIECES / 2
-                              ? p.g + (int64_t)q * p.gld  // G rows >= rows are zero
-                              : p.eps16.data + (int64_t)min(q, rows - 1) * p.eps16.ld;
+    const int q = q0 + (pc % (PIECES / 2)) * RPP;
+    const uint16_t* src;
+    int off = dma_off[i];
+    if (pc < PIECES / 2) {  // G rows >= rows are zero
+      src = p.g + (int64_t)q * p.gld;
+      off += lrow * p.gld * 2;
+    } else {  // E rows >= rows: repeat the last real row (finite, times a zero G row)
+      const int qb = min(q, rows - 1);
+      src = p.eps16.data + (int64_t)qb * p.eps16.ld;
+      off += (min(q + lrow, rows - 1) - qb) * (int)p.eps16.ld * 2;
+    }
     if (MPV_ABL & 128) continue;
     if (MPV_DMA_ASM)
-      lds_dma16(src, (uint32_t)dma_off[i], lds_addr(dst + pc * 1024));
+      lds_dma16(src, (uint32_t)off, lds_addr(dst + pc * 1024));
     else
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + dma_off[i],
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + off,
                                        (__attribute__((address_space(3))) void*)(dst + pc * 1024),
                                        16, 0, 0);
   }
@@ -433,15 +443,15 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
   // DMA lane mapping: RPP rows per 1-KB wave-instruction; wave w moves pieces
   // w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E rows.  Per-lane
   // byte offsets (without the stage's first row) of my pieces:
-  int dma_r[PER_WAVE], dma_off[PER_WAVE];
+  int dma_off[PER_WAVE];
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int pc = wid * PER_WAVE + i;
     const int pr = pc % (PIECES / 2);
     const int lrow = lane / (64 / RPP), lpos = lane % (64 / RPP);  // 16-B slot within the row
-    dma_r[i] = pr * RPP + lrow;  // K row within the stage
+    const int r = pr * RPP + lrow;  // K row within the stage
     const int u_lds = lpos >> 1, half = lpos & 1;
-    const int u_src = u_lds ^ (dma_r[i] & 7);
+    const int u_src = u_lds ^ (r & 7);
     dma_off[i] = 4 * (pc < PIECES / 2 ? l0 : z0) + u_src * 32 + half * 16;  // chunked: 4 B/column
   }
   // transposed-read lane mapping: lane 4q+p of its 16-lane group
@@ -456,7 +466,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
 
   const int nst = (q_end - q_begin + kDrKR - 1) / kDrKR;
   for (int j = 0; j < P && j < nst; ++j)
-    dr_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_r, dma_off);
+    dr_issue<PER_WAVE, PIECES, RPP>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_off);
   for (int ci = 0; ci < nst; ++ci) {
     MPV_STAMP(0);
     if (P == 1)
@@ -468,8 +478,8 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
     barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
     MPV_STAMP(2);
     if (ci + P < nst)
-      dr_issue<PER_WAVE, PIECES>(p, smem + ((ci + P) % kDrStages) * STAGE,
-                                 q_begin + (ci + P) * kDrKR, rows, wid, dma_r, dma_off);
+      dr_issue<PER_WAVE, PIECES, RPP>(p, smem + ((ci + P) % kDrStages) * STAGE,
+                                 q_begin + (ci + P) * kDrKR, rows, wid, dma_off);
     MPV_STAMP(3);
     const char* base = smem + (ci % kDrStages) * STAGE;
     s16x8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -640,7 +650,6 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
 template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   static_assert(WM == 2, "two wave groups");
-  constexpr int NW = WM * WN;
   constexpr int BL = WM * TM * 16, BZ = WN * TN * 16;
   static_assert(BL == BZ, "square tile: one LDS row layout for both operands");
   constexpr int ROWB = BL * 4;          // bytes per LDS row: BL columns, hi + lo
@@ -1166,6 +1175,7 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
 
 // ------------------------------------------------------------------- plans
 struct BwdPlan {
+  int dr_tile;                                  // dR output tile edge
   int TPR, RPI, nLc, nSc, rows_per_chunk;       // element pass
   int nLt, nZt, nKc, dr_rows_per_chunk, rows_pad;  // dR GEMM
   int64_t ldg;                                  // G plane columns (3xf16, padded)
@@ -1173,6 +1183,22 @@ struct BwdPlan {
 };
 
 constexpr int kDr16Tile = 256;  // 3xf16 dR tile: 256 x 256, 8 waves of 128 x 64
+// Small label / latent dims (both <= 128, e.g. mirflickr 38, nuswide 81): a
+// 128 x 128 tile (4 waves of 64 x 64, two workgroups per CU), so the G and
+// noise planes are padded to 128 columns instead of 256
+constexpr int kDr16TileSmall = 128;
+
+#ifndef MPV_DR_SMALL
+#define MPV_DR_SMALL 1  // 0: always the 256 tile (timing study)
+#endif
+#ifndef MPV_DR_SMALL_KC
+#define MPV_DR_SMALL_KC 2  // K chunks per CU for the 128 tile
+#endif
+
+static int dr16_tile(int64_t L, int64_t z) {
+  return (MPV_DR_SMALL && L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall
+                                                                       : kDr16Tile;
+}
 
 static int num_cus() {
   static int n = 0;
@@ -1190,7 +1216,8 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   BwdPlan pl;
   const int64_t L = s->L, S = s->S_local, B = s->B, z = s->z;
   const bool planes = gemm == MPV_GEMM_F16X3;
-  const int64_t dr_tile = planes ? kDr16Tile : 128;  // dR output tile edge
+  const int64_t dr_tile = planes ? dr16_tile(L, z) : 128;  // dR output tile edge
+  pl.dr_tile = (int)dr_tile;
   pl.ldg = cdiv(L, dr_tile) * dr_tile;
   const int64_t Lc = planes ? pl.ldg : L;  // columns the element pass covers
   pl.nLc = (int)cdiv(Lc, 1024);
@@ -1211,7 +1238,8 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.rows_pad = (int)(cdiv(rows, kr) * kr);
   // split-K chunks: the 3xf16 kernel (1 workgroup per CU) gets one workgroup
   // per CU in a single wave of equal chunks; the fp32 kernel several per CU
-  int64_t kc = planes ? cdiv(num_cus(), tiles) : cdiv(1536, tiles);
+  int64_t kc = planes ? cdiv((dr_tile == kDr16Tile ? 1 : MPV_DR_SMALL_KC) * (int64_t)num_cus(), tiles)
+                      : cdiv(1536, tiles);
   const int64_t kc_max = cdiv(rows, 256);
   if (kc > kc_max) kc = kc_max;
   if (kc < 1) kc = 1;
@@ -1238,6 +1266,12 @@ int mpv_dbg_dr_stamps(void* host_out) {
 }
 #endif
 
+int64_t mpv_noise_plane_cols(const mpv_shape* shape) {
+  if (check_shape(shape) != MPV_OK) return 0;
+  const int64_t t = dr16_tile(shape->L, shape->z);
+  return cdiv(shape->z, t) * t;
+}
+
 size_t mpv_bwd_workspace_bytes(const mpv_shape* shape, int gemm) {
   if (check_shape(shape) != MPV_OK) return 0;
   const BwdPlan pl = plan_bwd(shape, gemm);
@@ -1256,10 +1290,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   if (a->dR32) {
     if (planes) {
       MPV_REQUIRE(a->eps16.data && a->eps16.scale, "eps16 planes are NULL");
-      MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * kDr16Tile && a->eps16.ld % 64 == 0 &&
+      MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * pl.dr_tile && a->eps16.ld % 64 == 0 &&
                       a->eps16.rows_pad >= shape->S_local * shape->B,
-                  "eps16 planes too small (ld %lld < %lld)", (long long)a->eps16.ld,
-                  2 * (long long)pl.nZt * kDr16Tile);
+                  "eps16 planes too small (ld %lld < %lld: mpv_noise_plane_cols)",
+                  (long long)a->eps16.ld, 2 * (long long)pl.nZt * pl.dr_tile);
     } else {
       MPV_REQUIRE(a->eps != nullptr, "MPV_GEMM_F32 needs eps");
     }
@@ -1351,8 +1385,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.rows_per_chunk = pl.dr_rows_per_chunk;
       dp.rows_pad = pl.rows_pad;
       // 256 x 256 tile, 8 waves of 128 x 64, 2-stage ring (128 KB LDS)
-      static_assert(kDr16Tile == 256, "launch config below");
-      if (MPV_DR_KIND == 3)
+      static_assert(kDr16Tile == 256 && kDr16TileSmall == 128, "launch configs below");
+      if (pl.dr_tile == kDr16TileSmall)  // 128 x 128, 4 waves of 64 x 64, 2 x 32 KB stages
+        MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 4, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+      else if (MPV_DR_KIND == 3)
         MPV_LAUNCH("dR_gemm", (dR32s_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
       else if (MPV_DR_KIND == 2)
         MPV_LAUNCH("dR_gemm", (dR32_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);

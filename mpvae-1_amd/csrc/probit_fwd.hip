@@ -2153,7 +2153,7 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
           MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
         else
           if (MPV_FWD_LOAD)
-            MPV_LAUNCH("probit_fwd", probit_fwd16L_kernel<MPV_FWD_LOAD>, grid, dim3(768), 0, st, p);
+            MPV_LAUNCH("probit_fwd", (probit_fwd16L_kernel<MPV_FWD_LOAD ? MPV_FWD_LOAD : 2>), grid, dim3(768), 0, st, p);
           else if (MPV_FWD_TSA != 4 || MPV_FWD_PF)
             MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<MPV_FWD_TSA, 8 - MPV_FWD_TSA>), grid,
                        dim3(512), 0, st, p);

@@ -150,6 +150,32 @@ __global__ void sum_slabs_kernel(const float* __restrict__ in, int64_t nslab, in
   }
 }
 
+// Few columns over many slabs (small L x z, or the column partials): 16 waves
+// per workgroup split the slabs (wave g sums slabs g, g+16, ..., one coalesced
+// 256-B row each), then a fixed-order sum of the 16 partials through LDS: the
+// serial chain per lane is nslab/16 loads instead of nslab.
+template <typename D>
+__global__ __launch_bounds__(1024) void sum_slabs_split_kernel(const float* __restrict__ in,
+                                                               int64_t nslab, int64_t n,
+                                                               D* __restrict__ out) {
+  __shared__ float part[16][65];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  float acc = 0.0f;
+  if (i < n) {
+#pragma unroll 4
+    for (int64_t k = g; k < nslab; k += 16) acc += in[k * n + i];
+  }
+  part[g][lane] = acc;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = part[0][lane];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) t += part[j][lane];
+    out[i] = (D)t;
+  }
+}
+
 // gathered (R,6,B) -> out (6,B)
 __global__ void bstat_combine_kernel(const float* __restrict__ g, int64_t R, int64_t B,
                                      float* __restrict__ out) {
@@ -296,33 +322,32 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
   const int64_t e_row = ((s_off + ss) * B + bb) * (int64_t)z;  // first global element of the row
   const int cols = (int)(out.ld >> 1);
   for (int c0 = threadIdx.x * 4; c0 < cols; c0 += blockDim.x * 4) {
-    float v[4];
-    if ((z & 3) == 0) {
-      if (c0 < z) {
-        const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
-        const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
-        box_muller(w.x, w.y, v[0], v[1]);
-        box_muller(w.z, w.w, v[2], v[3]);
+    // Element e draws normal e & 3 of Philox counter e >> 2.  The row's first
+    // element is at phase sh (0 whenever z % 4 == 0; uniform over the row), so
+    // columns c0..c0+3 take normals sh..sh+3 of counters (e_row + c0) >> 2 and
+    // the next one: one Philox call when aligned, two otherwise.
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (c0 < z) {
+      const int sh = (int)(e_row & 3);
+      const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
+      const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+      float a[8];
+      box_muller(w.x, w.y, a[0], a[1]);
+      box_muller(w.z, w.w, a[2], a[3]);
+      if (sh == 0) {
+        v[0] = a[0], v[1] = a[1], v[2] = a[2], v[3] = a[3];
       } else {
-        v[0] = v[1] = v[2] = v[3] = 0.0f;
+        const uint64_t c2 = ctr + 1;
+        const u32x4 w2 = philox4x32_10(u32x4{(uint32_t)c2, (uint32_t)(c2 >> 32), 0u, 0u}, k0, k1);
+        box_muller(w2.x, w2.y, a[4], a[5]);
+        if (sh > 1) box_muller(w2.z, w2.w, a[6], a[7]);
+        if (sh == 1) v[0] = a[1], v[1] = a[2], v[2] = a[3], v[3] = a[4];
+        else if (sh == 2) v[0] = a[2], v[1] = a[3], v[2] = a[4], v[3] = a[5];
+        else v[0] = a[3], v[1] = a[4], v[2] = a[5], v[3] = a[6];
       }
-    } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = c0 + q;
-        v[q] = 0.0f;
-        if (c < z) {
-          const int64_t e = e_row + c;
-          const uint64_t ctr = (uint64_t)(e >> 2) + offset;
-          const u32x4 w =
-              philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
-          float n0, n1;
-          const int ln = (int)(e & 3);
-          if (ln < 2) box_muller(w.x, w.y, n0, n1);
-          else box_muller(w.z, w.w, n0, n1);
-          v[q] = (ln & 1) ? n1 : n0;
-        }
-      }
+      for (int q = 1; q < 4; ++q)
+        if (c0 + q >= z) v[q] = 0.0f;  // padding columns of the last group
     }
     uint16_t h[4], l[4];
 #pragma unroll
@@ -557,6 +582,16 @@ int launch_scale(const float* block_max, int n, float* scale, hipStream_t s) {
 
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
                      hipStream_t s) {
+  if (nslab >= 64 && n <= 256 * 256) {  // too few columns to hide the slab chain
+    const unsigned gs = (unsigned)((n + 63) / 64);
+    if (out_dtype == MPV_F64)
+      MPV_LAUNCH("sum_slabs", (sum_slabs_split_kernel<double>), dim3(gs), dim3(1024), 0, s, in,
+                 nslab, n, (double*)out);
+    else
+      MPV_LAUNCH("sum_slabs", (sum_slabs_split_kernel<float>), dim3(gs), dim3(1024), 0, s, in,
+                 nslab, n, (float*)out);
+    return check_launch("sum_slabs");
+  }
   const unsigned g = grid_for(n, 256, 8192);
   if (out_dtype == MPV_F64)
     MPV_LAUNCH("sum_slabs", (sum_slabs_kernel<double>), dim3(g), dim3(256), 0, s, in, nslab, n,

@@ -106,6 +106,7 @@ SIGNATURES = {
     "mpv_philox_raw": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, vp]),
     "mpv_convert": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int64, vp]),
     "mpv_split_workspace_bytes": (ctypes.c_size_t, []),
+    "mpv_noise_plane_cols": (ctypes.c_int64, [ctypes.POINTER(Shape)]),
     "mpv_split_f16": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
                                      ctypes.POINTER(Split16), vp, vp]),
     "mpv_noise_philox_f16": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.c_uint64,

@@ -54,7 +54,14 @@ class Planes:
 
 
 GEMMS = {"f16x3": H.GEMM_F16X3, "f32": H.GEMM_F32}
-EPS_PAD = 256  # noise plane columns: a whole number of 256-wide dR tiles (probit_bwd.hip)
+
+
+def eps_cols(shape):
+    """Noise plane columns: z padded to whole dR tiles (mpv_noise_plane_cols)."""
+    n = H.load_library().mpv_noise_plane_cols(shape)
+    if n <= 0:
+        raise H.MPVError("mpv_noise_plane_cols: bad shape")
+    return int(n)
 
 
 class HipShardBackend:
@@ -82,7 +89,7 @@ class HipShardBackend:
             raise ValueError("a device Philox seed must be a one-element int64 tensor on "
                              f"{device} (got {seed.dtype}, {seed.numel()} elements, {seed.device})")
         if self.gemm == H.GEMM_F16X3:
-            eps = Planes(shape.S_local * shape.B, _pad(shape.z, EPS_PAD), device)
+            eps = Planes(shape.S_local * shape.B, eps_cols(shape), device)
             if dev_key:
                 H.check(lib.mpv_noise_philox_f16_dev(shape, H.ptr(seed), offset, eps.c(), st),
                         "mpv_noise_philox_f16_dev")
@@ -113,7 +120,7 @@ class HipShardBackend:
         rows = shape.S_local * shape.B
         # plane rows are b-major (row b*S + s): split the (B, S, z) transpose
         eps_bs = eps.transpose(0, 1).contiguous()
-        return self._split(eps_bs, rows, shape.z, Planes(rows, _pad(shape.z, EPS_PAD), eps.device))
+        return self._split(eps_bs, rows, shape.z, Planes(rows, eps_cols(shape), eps.device))
 
     def prepare_R(self, R):
         """r_sqrt_sigma (L,z) fp64/fp32 -> the GEMM operand (R.T.float(), mpvae.py:165)."""

@@ -92,7 +92,8 @@ def test_philox_kernel_known_answers():
     assert got == want
 
 
-@pytest.mark.parametrize("S,B,z,s_off", [(7, 5, 13, 0), (9, 3, 38, 5), (64, 16, 128, 100)])
+@pytest.mark.parametrize("S,B,z,s_off", [(7, 5, 13, 0), (9, 3, 38, 5), (5, 6, 7, 3), (11, 4, 81, 2),
+                                         (64, 16, 128, 100), (3, 2, 131, 1)])
 def test_philox_noise_matches_oracle(S, B, z, s_off):
     shape = H.Shape(S, s_off + S, s_off, B, 4, z)
     ref = philox.normal_noise(S, B, z, seed=0x1234ABCD5678, s_offset=s_off)
