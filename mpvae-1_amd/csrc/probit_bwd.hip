@@ -23,6 +23,9 @@
 #ifndef MPV_ABL
 #define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
 #endif
+#ifndef MPV_ELEM_NT
+#define MPV_ELEM_NT 3  // nontemporal 1: T loads, 2: G-plane stores (both: element pass -5 %)
+#endif
 
 namespace mpv {
 
@@ -177,7 +180,9 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   r.bN = f32x2{p.coef[2 * BS + cb], p.coef[5 * BS + cb]};
   const float* row = p.T + cb * p.L;
   if (VEC && c0 + 3 < p.L) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(row + c0);
+    const f32x4 v = (MPV_ELEM_NT & 1)
+                        ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0))
+                        : *reinterpret_cast<const f32x4*>(row + c0);
     r.t[0] = v[0]; r.t[1] = v[1]; r.t[2] = v[2]; r.t[3] = v[3];
   } else {
 #pragma unroll
@@ -269,9 +274,15 @@ __global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams 
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
         // rows b*S + s (the noise planes' row order), chunked like mpv_split16
         const int64_t o = chunked_index(cb, p.gld, c0);
-        *reinterpret_cast<s16x4*>(p.g + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-        *reinterpret_cast<s16x4*>(p.g + o + kLoOff) =
-            s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+        const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+        const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+        if (MPV_ELEM_NT & 2) {
+          __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
+          __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
+        } else {
+          *reinterpret_cast<s16x4*>(p.g + o) = hv;
+          *reinterpret_cast<s16x4*>(p.g + o + kLoOff) = lv;
+        }
       } else {
         float* row = p.T + cb * L;
         if (VEC && c0 + 3 < L) {

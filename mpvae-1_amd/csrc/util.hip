@@ -310,6 +310,9 @@ constexpr float kNoiseScale = 4096.0f;
 #ifndef MPV_NOISE_ROWS
 #define MPV_NOISE_ROWS 16  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
 #endif
+#ifndef MPV_NOISE_NT
+#define MPV_NOISE_NT 0  // study: nontemporal stores of the noise planes (+38 %, off)
+#endif
 __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
                                                             int z, int64_t s_off, uint32_t k0,
                                                             uint32_t k1, uint64_t offset,
@@ -353,9 +356,15 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
 #pragma unroll
     for (int q = 0; q < 4; ++q) split_f16(v[q], kNoiseScale, h[q], l[q]);
     const int64_t o = chunked_index(r, out.ld, c0);
-    *reinterpret_cast<s16x4*>(out.data + o) = s16x4{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-    *reinterpret_cast<s16x4*>(out.data + o + kLoOff) =
-        s16x4{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+    const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+    const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+    if (MPV_NOISE_NT) {
+      __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(out.data + o));
+      __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(out.data + o + kLoOff));
+    } else {
+      *reinterpret_cast<s16x4*>(out.data + o) = hv;
+      *reinterpret_cast<s16x4*>(out.data + o + kLoOff) = lv;
+    }
   }
   }
 }

@@ -2,7 +2,7 @@
 # Timing ablations of the GEMM kernels: builds libmpvae_hip.so variants into
 # abl/<variant>/ (here: `build`) and times them on the GPU box (`run`).
 # A variant is <bits>[:<extra>...]: <bits> = MPV_ABL (probit_fwd.hip /
-# probit_bwd.hip); each ':'-separated extra is MACRO=value (-D) or a raw -flag.
+# probit_bwd.hip / util.hip); each ':'-separated extra is MACRO=value (-D) or a raw -flag.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 VARIANTS="${VARIANTS:-0 1 5 9 17 13 25}"
 dir_of() { echo "$R/abl/$(echo "$1" | tr ':=' '__' | tr -d ' ')"; }
@@ -16,7 +16,7 @@ case "$1" in
         IFS=':' read -ra parts <<< "${v#*:}"
         for x in "${parts[@]}"; do [[ "$x" == -* ]] && extra="$extra $x" || extra="$extra -D$x"; done
       fi
-      for f in probit_fwd probit_bwd; do
+      for f in probit_fwd probit_bwd util; do
         /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -Icsrc \
           -DMPV_ABL=$bits $extra -c csrc/$f.hip -o "$d/$f.o" &
       done
@@ -25,8 +25,8 @@ case "$1" in
     for v in $VARIANTS; do
       d=$(dir_of "$v")
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined \
-        -o "$d/libmpvae_hip.so" "$d/probit_fwd.o" "$d/probit_bwd.o" \
-        $(ls build/*.o | grep -v "build/probit_") || exit 1
+        -o "$d/libmpvae_hip.so" "$d/probit_fwd.o" "$d/probit_bwd.o" "$d/util.o" \
+        $(ls build/*.o | grep -v "build/probit_\|build/util.o") || exit 1
     done ;;
   run)
     mkdir -p "$R/gpurun_out/abl"
