@@ -203,6 +203,9 @@ RANDOM_CASES = [
     (38, 38, 128, 100, 50),      # C2 shape at S/10
     (81, 81, 16, 200, 50),       # C3 label dim
     (100, 37, 3, 130, 8),        # z % 4 != 0, ragged everything
+    (128, 5, 3, 70, 8),          # 128 x 128 dR tile at its edge, z < 16
+    (2, 100, 4, 33, 8),          # two labels
+    (129, 128, 2, 50, 8),        # one label past the small tile: 256 tile
     (200, 64, 5, 257, 8),        # two column tiles, ragged s tiles
     (1024, 1024, 2, 48, 50),     # C4 dims, tiny batch
     (1030, 96, 2, 20, 8),        # L > 1024: two bwd column chunks
