@@ -172,10 +172,18 @@ constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free 
 
 // Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
+#ifndef MPV_FWD_MAP
+#define MPV_FWD_MAP 0  // study: 1 = blocks of one XCD share the label tile (R slice) instead of the row group (+5 %)
+#endif
 MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
   const int full = (G / 8) * 8 * nNt;
   if (id < full) {
     const int q = id / (8 * nNt), r = id % (8 * nNt);
+    if (MPV_FWD_MAP) {
+      nt = r % nNt;
+      g = q * 8 + r / nNt;
+      return;
+    }
     nt = r / 8;
     g = q * 8 + (r % 8);
   } else {
