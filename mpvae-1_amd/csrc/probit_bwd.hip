@@ -196,6 +196,9 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
 #ifndef MPV_ELEM_LA
 #define MPV_ELEM_LA 1
 #endif
+#ifndef MPV_ELEM_MINR
+#define MPV_ELEM_MINR 16  // minimum T rows per thread of the element pass (C2 -6 %; 0: no minimum)
+#endif
 #ifndef MPV_ELEM_WPS
 #define MPV_ELEM_WPS 4  // minimum waves per SIMD the element pass is compiled for (128 VGPRs)
 #endif
@@ -1236,6 +1239,8 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.RPI = 256 / pl.TPR;
   // s-chunks: enough blocks for several rounds of resident blocks (short tail)
   int64_t want = cdiv(8192, B * pl.nLc);
+  if (MPV_ELEM_MINR > 0)  // but at least MPV_ELEM_MINR rows per thread (block setup amortised)
+    want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * MPV_ELEM_MINR));
   if (want < 1) want = 1;
   const int64_t max_chunks = cdiv(S, pl.RPI);
   if (want > max_chunks) want = max_chunks;
