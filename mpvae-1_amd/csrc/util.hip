@@ -304,27 +304,23 @@ __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int
 // the constant 2^12 (max |n| * s < 24200 < 65504).
 constexpr float kNoiseScale = 4096.0f;
 
-// One block per plane row r = b*S + s; a thread makes 4 consecutive columns.
-// With z % 4 == 0 those are the 4 words of ONE Philox call (2 Box-Muller
-// pairs); otherwise each column picks its word from the call covering it.
+// A block makes MPV_NOISE_ROWS plane rows r = b*S + s; a thread makes 4
+// consecutive columns at a time (the 4 words of ONE Philox call when z % 4 ==
+// 0, else words of two calls).  Planes narrower than 4 x blockDim columns
+// give each row cols/4 threads and the block several rows at once.
 #ifndef MPV_NOISE_ROWS
 #define MPV_NOISE_ROWS 16  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
 #endif
 #ifndef MPV_NOISE_NT
 #define MPV_NOISE_NT 0  // study: nontemporal stores of the noise planes (+38 %, off)
 #endif
-__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
-                                                            int z, int64_t s_off, uint32_t k0,
-                                                            uint32_t k1, uint64_t offset,
-                                                            int rows,
-                                                            const uint64_t* __restrict__ seed_dev) {
-  philox_key(seed_dev, k0, k1);
-  const int r_end = min(rows, (int)(blockIdx.x + 1) * MPV_NOISE_ROWS);
-  for (int r = blockIdx.x * MPV_NOISE_ROWS; r < r_end; ++r) {
+// Columns c_first, c_first + c_step, ... (4 each) of plane row r.
+MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_off, uint32_t k0,
+                         uint32_t k1, uint64_t offset, int r, int c_first, int c_step) {
   const int bb = r / S, ss = r - bb * S;
   const int64_t e_row = ((s_off + ss) * B + bb) * (int64_t)z;  // first global element of the row
   const int cols = (int)(out.ld >> 1);
-  for (int c0 = threadIdx.x * 4; c0 < cols; c0 += blockDim.x * 4) {
+  for (int c0 = c_first; c0 < cols; c0 += c_step) {
     // Element e draws normal e & 3 of Philox counter e >> 2.  The row's first
     // element is at phase sh (0 whenever z % 4 == 0; uniform over the row), so
     // columns c0..c0+3 take normals sh..sh+3 of counters (e_row + c0) >> 2 and
@@ -366,6 +362,25 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
       *reinterpret_cast<s16x4*>(out.data + o + kLoOff) = lv;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
+                                                            int z, int64_t s_off, uint32_t k0,
+                                                            uint32_t k1, uint64_t offset,
+                                                            int rows,
+                                                            const uint64_t* __restrict__ seed_dev) {
+  philox_key(seed_dev, k0, k1);
+  const int cols = (int)(out.ld >> 1);
+  const int r_end = min(rows, (int)(blockIdx.x + 1) * MPV_NOISE_ROWS);
+  const int tpr = min((int)blockDim.x, cols >> 2);  // threads per row
+  if (tpr == (int)blockDim.x) {  // wide planes: the row (and its index math) is block-uniform
+    for (int r = blockIdx.x * MPV_NOISE_ROWS; r < r_end; ++r)
+      noise16_row(out, S, B, z, s_off, k0, k1, offset, r, threadIdx.x * 4, blockDim.x * 4);
+  } else {  // narrow planes (C2, C3): several rows per pass of the block
+    const int rpi = (int)blockDim.x / tpr;
+    if ((int)threadIdx.x >= rpi * tpr) return;
+    for (int r = blockIdx.x * MPV_NOISE_ROWS + (int)threadIdx.x / tpr; r < r_end; r += rpi)
+      noise16_row(out, S, B, z, s_off, k0, k1, offset, r, ((int)threadIdx.x % tpr) * 4, tpr * 4);
   }
 }
 
