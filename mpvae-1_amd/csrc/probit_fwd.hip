@@ -172,6 +172,9 @@ constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free 
 
 // Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
+#ifndef MPV_FWD_CFG
+#define MPV_FWD_CFG -1  // study: force the tile configuration of a 3xf16 forward with L <= 128
+#endif
 #ifndef MPV_FWD_MAP
 #define MPV_FWD_MAP 0  // study: 1 = blocks of one XCD share the label tile (R slice) instead of the row group (+5 %)
 #endif
@@ -2119,7 +2122,11 @@ struct FwdPlan {
 static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
   const bool wide = MPV_FWD_WIDE && gemm == MPV_GEMM_F16X3 && s->L > 128;
-  pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : (wide ? 3 : 2));
+  // 3xf16 with 48 < L <= 96: the 128 x 128 transposed tile beats the 96-label
+  // one in spite of its pad labels (C3, L = 81: forward 0.216 -> 0.167 ms)
+  const bool f16 = gemm == MPV_GEMM_F16X3;
+  pl.cfg = s->L <= 48 ? 0 : ((s->L <= 96 && !f16) ? 1 : (wide ? 3 : 2));
+  if (MPV_FWD_CFG >= 0 && f16 && s->L <= 128) pl.cfg = MPV_FWD_CFG;
   pl.BM = (pl.cfg == 3 && MPV_FWD_BIG) ? 256 : 128;
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
@@ -2153,7 +2160,7 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 0:  // BN 48, 4 waves, 3-stage ring (66 KB LDS: 2 workgroups per CU)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 3>), grid, dim3(256), 0, st, p);
         break;
-      case 1:  // BN 96, 8 waves, 4-stage ring (112 KB)
+      case 1:  // BN 96, 8 waves, 4-stage ring (112 KB); study only (MPV_FWD_CFG=1)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
         break;
       case 3:  // 256 labels x 128 samples, 8 waves of 64 x 64, one workgroup per CU
