@@ -130,7 +130,7 @@ typedef struct mpv_fwd_args {
   const float* R32;     /* MPV_GEMM_F32:   (L,z) fp32 */
   const float* eps;     /*                 (S_local,B,z) fp32 */
   mpv_split16 R16;      /* MPV_GEMM_F16X3: R planes, rows_pad >= roundup(L,256), ld >= 2*roundup(z,128) */
-  mpv_split16 eps16;    /*                 noise planes, row b*S_local + s = eps[s, b, :], ld >= 2*roundup(z,256) */
+  mpv_split16 eps16;    /*                 noise planes, row b*S_local + s = eps[s, b, :], ld >= 2*mpv_noise_plane_cols() */
   float* T;             /* (B,S_local,L) or NULL when no backward will follow */
   float* rowstat;       /* (6,B,S_local) out */
   float* bstat;         /* (6,B) out: this shard's statistics */
