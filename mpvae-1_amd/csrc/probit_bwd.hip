@@ -196,6 +196,9 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
 #ifndef MPV_ELEM_LA
 #define MPV_ELEM_LA 1
 #endif
+#ifndef MPV_ELEM_ST16
+#define MPV_ELEM_ST16 0  // study: G planes as 16-B stores through a DPP swap of lane pairs (+3.5 %, off)
+#endif
 #ifndef MPV_ELEM_MINR
 #define MPV_ELEM_MINR 16  // minimum T rows per thread of the element pass (C2 -6 %; 0: no minimum)
 #endif
@@ -279,7 +282,28 @@ __global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams 
         const int64_t o = chunked_index(cb, p.gld, c0);
         const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
         const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
-        if (MPV_ELEM_NT & 2) {
+        if (MPV_ELEM_ST16) {
+          // lanes 2i, 2i+1 hold columns c0, c0 + 4 of one 8-column run (TPR is
+          // a multiple of 32 on the planes path): one DPP swap hands the even
+          // lane the odd lane's hi words and the odd lane the even lane's lo,
+          // so each stores 16 B (the run's 8 hi or 8 lo halves) instead of 2 x 8
+          const bool odd = (cq & 1) != 0;
+          const uint32_t hw0 = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+          const uint32_t hw1 = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+          const uint32_t lw0 = (uint32_t)l[0] | ((uint32_t)l[1] << 16);
+          const uint32_t lw1 = (uint32_t)l[2] | ((uint32_t)l[3] << 16);
+          const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(
+              0, (int)(odd ? hw0 : lw0), 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+          const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(
+              0, (int)(odd ? hw1 : lw1), 0xB1, 0xF, 0xF, false);
+          typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
+          const u32v4 v = odd ? u32v4{r0, r1, lw0, lw1} : u32v4{hw0, hw1, r0, r1};
+          const int64_t o8 = chunked_index(cb, p.gld, c0 & ~7) + (odd ? kLoOff : 0);
+          if (MPV_ELEM_NT & 2)
+            __builtin_nontemporal_store(v, reinterpret_cast<u32v4*>(p.g + o8));
+          else
+            *reinterpret_cast<u32v4*>(p.g + o8) = v;
+        } else if (MPV_ELEM_NT & 2) {
           __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
           __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
         } else {
