@@ -172,6 +172,9 @@ constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free 
 
 // Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
+#ifndef MPV_FWD_WANT
+#define MPV_FWD_WANT 2048  // target workgroup count of the forward grid (s-chunking; 4096-16384: ±0.5 %)
+#endif
 #ifndef MPV_FWD_CFG
 #define MPV_FWD_CFG -1  // study: force the tile configuration of a 3xf16 forward with L <= 128
 #endif
@@ -2132,7 +2135,7 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
   // enough workgroups to fill 256 CUs several times; fewer s-chunks = fewer partials
-  int64_t want = cdiv(2048, s->B * (int64_t)pl.nNt);
+  int64_t want = cdiv(MPV_FWD_WANT, s->B * (int64_t)pl.nNt);
   if (want < 1) want = 1;
   if (want > pl.nSt) want = pl.nSt;
   pl.tps = (int)cdiv(pl.nSt, want);
