@@ -450,6 +450,30 @@ MPV_DEV void lds_dma16(const void* saddr, uint32_t voff, uint32_t lds) {
       : "memory");
 }
 
+// lds_dma16 with a cache policy on the load (study): POL bits 1 sc0, 2 sc1, 4 nt.
+template <int POL>
+MPV_DEV void lds_dma16_pol(const void* saddr, uint32_t voff, uint32_t lds) {
+  if constexpr (POL == 0) {
+    lds_dma16(saddr, voff, lds);
+  } else {
+    uint32_t keep;
+#define MPV_DMA_ASM_POL(MOD)                                              \
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"        \
+               "global_load_lds_dwordx4 %1, %2" MOD "\n\ts_mov_b32 m0, %0" \
+               : "=&s"(keep)                                              \
+               : "v"(voff), "s"(saddr), "s"(lds)                          \
+               : "memory")
+    if constexpr (POL == 1) MPV_DMA_ASM_POL(" sc0");
+    else if constexpr (POL == 2) MPV_DMA_ASM_POL(" sc1");
+    else if constexpr (POL == 3) MPV_DMA_ASM_POL(" sc0 sc1");
+    else if constexpr (POL == 4) MPV_DMA_ASM_POL(" nt");
+    else if constexpr (POL == 5) MPV_DMA_ASM_POL(" sc0 nt");
+    else if constexpr (POL == 6) MPV_DMA_ASM_POL(" sc1 nt");
+    else MPV_DMA_ASM_POL(" sc0 sc1 nt");
+#undef MPV_DMA_ASM_POL
+  }
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n (the immediate must be a constant).
 MPV_DEV void wait_vmcnt_dyn(int n) {
 #define MPV_VMC(k) \

@@ -172,6 +172,12 @@ constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free 
 
 // Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
+#ifndef MPV_FWD_POL_A
+#define MPV_FWD_POL_A 0  // study: cache policy of the eps-image DMA (lds_dma16_pol)
+#endif
+#ifndef MPV_FWD_POL_B
+#define MPV_FWD_POL_B 0  // study: cache policy of the R-image DMA (nt: +7.5 %)
+#endif
 #ifndef MPV_FWD_WANT
 #define MPV_FWD_WANT 2048  // target workgroup count of the forward grid (s-chunking; 4096-16384: ±0.5 %)
 #endif
@@ -623,9 +629,10 @@ struct Fwd16Dma {
   }
 
   // base: wave-uniform (SGPRs); off: per-lane byte offset (inline-asm DMA, see lds_dma16)
+  template <int POL = 0>
   MPV_DEV static void piece(const char* base, uint32_t off, char* dst) {
     if (MPV_ABL & 4) return;
-    lds_dma16(base, off, lds_addr(dst));
+    lds_dma16_pol<POL>(base, off, lds_addr(dst));
   }
 
   // Stream the next stage (if any) into stage image `dst` (PART 1: only the
@@ -638,14 +645,14 @@ struct Fwd16Dma {
 #pragma unroll
       for (int j = 0; j < JA; ++j) {
         const int pc = wid + j * NW;
-        if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[j], dst + pc * 1024);
+        if (GA % NW == 0 || pc < GA) piece<MPV_FWD_POL_A>(a_base + kb, offa[j], dst + pc * 1024);
       }
     }
     if (PART != 1) {
 #pragma unroll
       for (int j = 0; j < JB; ++j) {
         const int pc = wid + j * NW;
-        if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
+        if (GB % NW == 0 || pc < GB) piece<MPV_FWD_POL_B>(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
       }
     }
     ++issued;
