@@ -80,6 +80,9 @@ struct FwdParams {
 #ifndef MPV_T_NT
 #define MPV_T_NT 0
 #endif
+#ifndef MPV_T_SC1
+#define MPV_T_SC1 0  // study: T stash with sc1 stores (lines leave the XCD's L2): +4 %, off
+#endif
 // forward with the epilogue pipelined into the next tile's K loop
 // (probit_fwd16p_kernel; study, off): parity-correct, but 18.6 ms (1 VALU
 // filler per MFMA) / 20.2 ms (2) / 29.9 ms (no interleave) against 14.5 ms:
@@ -987,7 +990,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
           const int lb = (wl * TL + m) * 16 + lg * 4;
           const f32x4 t4 = acc[m][n];
           if (vecT && n0 + lb + 3 < L) {
-            if (MPV_T_NT)
+            if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
+              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(t4)
+                           : "memory");
+            else if (MPV_T_NT)
               __builtin_nontemporal_store(t4, reinterpret_cast<f32x4*>(row + lb));
             else
               *reinterpret_cast<f32x4*>(row + lb) = t4;
@@ -1046,7 +1052,11 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         if (s >= s_own && s < S) {
           float* row = p.T + ((int64_t)b * S + s) * L + n0;
           if ((L & 3) == 0 && n0 + lb + 3 < L) {
-            *reinterpret_cast<f32x4*>(row + lb) = am[n];
+            if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
+              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(am[n])
+                           : "memory");
+            else
+              *reinterpret_cast<f32x4*>(row + lb) = am[n];
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
