@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 4  /* 4: device-memory Philox keys (mpv_noise_philox*_dev) */
+#define MPV_ABI_VERSION 5  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+                              5: T rows padded to roundup(L, 4) floats */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -131,7 +132,8 @@ typedef struct mpv_fwd_args {
   const float* eps;     /*                 (S_local,B,z) fp32 */
   mpv_split16 R16;      /* MPV_GEMM_F16X3: R planes, rows_pad >= roundup(L,256), ld >= 2*roundup(z,128) */
   mpv_split16 eps16;    /*                 noise planes, row b*S_local + s = eps[s, b, :], ld >= 2*mpv_noise_plane_cols() */
-  float* T;             /* (B,S_local,L) or NULL when no backward will follow */
+  float* T;             /* (B,S_local,roundup(L,4)): rows 16-B aligned, the pad columns
+                           scratch; or NULL when no backward will follow */
   float* rowstat;       /* (6,B,S_local) out */
   float* bstat;         /* (6,B) out: this shard's statistics */
   float* colsum;        /* (2,B,L) out: this shard's sums over s */

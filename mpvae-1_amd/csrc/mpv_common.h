@@ -450,6 +450,11 @@ MPV_DEV void lds_dma16(const void* saddr, uint32_t voff, uint32_t lds) {
       : "memory");
 }
 
+// Row stride (floats) of T and of the fp32 G written over it: L rounded up to
+// 4, so every row starts 16-B aligned and the element pass reads whole float4
+// (ABI v5; include/mpvae_hip.h).
+__host__ __device__ inline int64_t t_cols(int64_t L) { return (L + 3) & ~int64_t(3); }
+
 // lds_dma16 with a cache policy on the load (study): POL bits 1 sc0, 2 sc1, 4 nt.
 template <int POL>
 MPV_DEV void lds_dma16_pol(const void* saddr, uint32_t voff, uint32_t lds) {

@@ -99,12 +99,13 @@ struct ElemParams {
   const float* gI;   // (B,L) grad of indiv_prob (feature branch) or NULL
   const float* gIL;  // (B,L) grad of indiv_prob_label (label branch) or NULL
   const float* coef;
-  float* T;
+  float* T;          // (B*S, ldT)
   uint16_t* g;       // chunked 3xf16 output planes (B*S rows of gld halves), or NULL: fp32 G over T
   const float* g_scale;
   int64_t gld;
   float* colpart;  // [nSc][2][B][L]
   int S, B, L, Lc;  // Lc: columns covered (L, or gld/2 for planes: pads get zeros)
+  int ldT;          // t_cols(L)
   int TPR, RPI, rows_per_chunk;
   float inv_S;
 };
@@ -178,8 +179,8 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   r.alpha = f32x2{p.coef[0 * BS + cb], p.coef[3 * BS + cb]};
   r.bP = f32x2{p.coef[1 * BS + cb], p.coef[4 * BS + cb]};
   r.bN = f32x2{p.coef[2 * BS + cb], p.coef[5 * BS + cb]};
-  const float* row = p.T + cb * p.L;
-  if (VEC && c0 + 3 < p.L) {
+  const float* row = p.T + cb * p.ldT;
+  if (VEC && c0 < p.L) {  // t_cols rows: the pad columns are readable
     const f32x4 v = (MPV_ELEM_NT & 1)
                         ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0))
                         : *reinterpret_cast<const f32x4*>(row + c0);
@@ -311,8 +312,8 @@ __global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams 
           *reinterpret_cast<s16x4*>(p.g + o + kLoOff) = lv;
         }
       } else {
-        float* row = p.T + cb * L;
-        if (VEC && c0 + 3 < L) {
+        float* row = p.T + cb * p.ldT;
+        if (VEC && c0 < L) {  // pad columns get G = 0
           *reinterpret_cast<f32x4*>(row + c0) = f32x4{G[0], G[1], G[2], G[3]};
         } else {
 #pragma unroll
@@ -1063,10 +1064,11 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR32s_kernel(Dr16Params p) {
 
 // ---------------------------------------------------------------- dR GEMM
 struct DrParams {
-  const float* G;    // (B*S, L): row q = b*S + s  (the T buffer)
+  const float* G;    // (B*S, ldG): row q = b*S + s  (the T buffer)
   const float* eps;  // (S, B, z)
   float* slab;       // [nKc][L][z]
   int S, B, L, z;
+  int ldG;  // t_cols(L)
   int nLt, nZt, nKc, rows_per_chunk;
 };
 
@@ -1108,7 +1110,7 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
   const int rows = B * S;
   const int q_begin = kc * p.rows_per_chunk;
   const int q_end = min(rows, q_begin + p.rows_per_chunk);
-  const bool gvec = (L & 3) == 0, evec = (z & 3) == 0;
+  const bool gvec = true, evec = (z & 3) == 0;  // G rows: t_cols stride
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -1126,8 +1128,8 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
         const int r = idx / (BM / 4), c = l0 + (idx % (BM / 4)) * 4;
         const int q = q0 + r;
         if (q < q_end) {
-          const float* src = p.G + (int64_t)q * L;
-          if (gvec && c + 3 < L) x = *reinterpret_cast<const f32x4*>(src + c);
+          const float* src = p.G + (int64_t)q * p.ldG;
+          if (gvec && c < L) x = *reinterpret_cast<const f32x4*>(src + c);  // pads hold G = 0
           else {
 #pragma unroll
             for (int k = 0; k < 4; ++k) x[k] = (c + k < L) ? src[c + k] : 0.0f;
@@ -1385,13 +1387,14 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.S = S;
   ep.B = B;
   ep.L = L;
+  ep.ldT = (int)t_cols(L);
   ep.Lc = want_planes ? (int)pl.ldg : L;
   ep.TPR = pl.TPR;
   ep.RPI = pl.RPI;
   ep.rows_per_chunk = pl.rows_per_chunk;
   ep.inv_S = 1.0f / (float)shape->S_total;
   const dim3 eg(B, pl.nSc, pl.nLc);
-  const bool vec = (L & 3) == 0;
+  const bool vec = true;  // t_cols rows (the scalar instantiations stay for study)
   if (want_planes) {
     if (vec && pl.RPI == 1)
       MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, true>), eg, dim3(256), 0, st, ep);
@@ -1444,6 +1447,7 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.S = S;
       dp.B = B;
       dp.L = L;
+      dp.ldG = (int)t_cols(L);
       dp.z = z;
       dp.nLt = pl.nLt;
       dp.nZt = pl.nZt;

@@ -37,10 +37,11 @@ struct FwdParams {
   const float* eps;  // fp32 mode
   mpv_split16 R16;   // 3xf16 mode
   mpv_split16 eps16;
-  float* T;
+  float* T;        // (B, S, ldT)
   float* rowpart;  // [6][nNt][B][S]
   float* colpart;  // [nSc][2][B][L]
   int S, B, L, z;
+  int ldT;  // t_cols(L)
   int nNt, nSc, tps, nSt;
 };
 
@@ -342,7 +343,7 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
       for (int n = 0; n < TN; ++n) {
         const bool ok = rowok && cl.colok[n];
         const float t = acc[m][n][i] * scale;
-        if (!(MPV_ABL & 2) && p.T != nullptr && ok) p.T[((int64_t)b * S + s) * L + cl.col[n]] = t;
+        if (!(MPV_ABL & 2) && p.T != nullptr && ok) p.T[((int64_t)b * S + s) * p.ldT + cl.col[n]] = t;
         f32x2 phi;
         const f32x2 E = probit_eval2(splat2(t) + f32x2{cl.fe[n], cl.fx[n]}, phi);
         const float y = cl.y[n];
@@ -979,17 +980,17 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // x TL groups cover whole 128-B lines of the sample's T row (written while
   // still combinable in L2, rather than as half lines far apart in time)
   if (!(MPV_ABL & 2) && !MPV_T_SPLIT && p.T != nullptr) {
-    const bool vecT = (L & 3) == 0;
+    const bool vecT = true;  // t_cols rows: 16-B aligned, pad labels (t = 0) may be written
 #pragma unroll
     for (int n = 0; n < TS; ++n) {
       const int s = s0 + (sbo + n) * 16 + lr;
       if (s >= s_own && s < S) {
-        float* row = p.T + ((int64_t)b * S + s) * L + n0;
+        float* row = p.T + ((int64_t)b * S + s) * p.ldT + n0;
 #pragma unroll
         for (int m = 0; m < TL; ++m) {
           const int lb = (wl * TL + m) * 16 + lg * 4;
           const f32x4 t4 = acc[m][n];
-          if (vecT && n0 + lb + 3 < L) {
+          if (vecT && n0 + lb < L) {
             if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
               asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(t4)
                            : "memory");
@@ -1050,8 +1051,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       for (int n = 0; n < TS; ++n) {
         const int s = s0 + (sbo + n) * 16 + lr;
         if (s >= s_own && s < S) {
-          float* row = p.T + ((int64_t)b * S + s) * L + n0;
-          if ((L & 3) == 0 && n0 + lb + 3 < L) {
+          float* row = p.T + ((int64_t)b * S + s) * p.ldT + n0;
+          if (n0 + lb < L) {  // t_cols rows: the pad labels' t (0) may be written
             if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
               asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(am[n])
                            : "memory");
@@ -1912,7 +1913,7 @@ MPV_DEV void fwdp_main(const FwdParams& p) {
     const int s = prev_s0 + (ws * TS + n) * 16 + lr;
     const int lb = (wl * TL + mg) * 16 + lg * 4;
     if (s >= prev_own && s < S && n0 + lb < L)
-      *reinterpret_cast<f32x4*>(p.T + ((int64_t)b * S + s) * L + n0 + lb) = t4;
+      *reinterpret_cast<f32x4*>(p.T + ((int64_t)b * S + s) * p.ldT + n0 + lb) = t4;
   };
 
   bool have_prev = false;
@@ -2285,6 +2286,7 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   p.S = (int)shape->S_local;
   p.B = (int)shape->B;
   p.L = (int)shape->L;
+  p.ldT = (int)t_cols(shape->L);
   p.z = (int)shape->z;
   p.nNt = pl.nNt;
   p.nSc = pl.nSc;

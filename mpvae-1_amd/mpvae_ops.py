@@ -155,7 +155,8 @@ class HipShardBackend:
         lib = H.load_library()
         dev = y.device
         S, B, L = shape.S_local, shape.B, shape.L
-        T = torch.empty((B, S, L), device=dev, dtype=torch.float32) if keep_T else None
+        # rows padded to 4 floats (ABI v5: 16-B aligned rows for the element pass)
+        T = torch.empty((B, S, (L + 3) // 4 * 4), device=dev, dtype=torch.float32) if keep_T else None
         rowstat = torch.empty((6, B, S), device=dev, dtype=torch.float32)
         bstat = torch.empty((6, B), device=dev, dtype=torch.float32)
         colsum = torch.empty((2, B, L), device=dev, dtype=torch.float32)
