@@ -364,6 +364,25 @@ MPV_DEV float block_reduce(float v, float* red) {
   return r;
 }
 
+// Two block reductions of the same kind at the cost of one (`red` >= 32
+// floats); each value is combined in the same order as by block_reduce.
+template <bool IS_MAX>
+MPV_DEV void block_reduce2(float& a, float& b, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  a = IS_MAX ? wave_max(a) : wave_sum(a);
+  b = IS_MAX ? wave_max(b) : wave_sum(b);
+  __syncthreads();
+  if (lane == 0) red[wid] = a, red[16 + wid] = b;
+  __syncthreads();
+  float ra = IS_MAX ? -INFINITY : 0.0f, rb = ra;
+  for (int i = 0; i < nw; ++i) {
+    ra = IS_MAX ? fmaxf(ra, red[i]) : ra + red[i];
+    rb = IS_MAX ? fmaxf(rb, red[16 + i]) : rb + red[16 + i];
+  }
+  a = ra, b = rb;
+}
+
 // ---- 3xf16 split operands ---------------------------------------------------
 // x*s = hi + lo with hi = fp16(x*s), lo = fp16(x*s - hi); the power-of-two
 // scale s keeps max|x*s| <= 2^15 so both halves stay in the fp16 normal range

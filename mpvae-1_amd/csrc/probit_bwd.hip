@@ -46,7 +46,7 @@ __global__ __launch_bounds__(1024) void bwd_coef_kernel(
     const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
     float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
     float nll_coeff, float c_coeff, int live) {
-  __shared__ float red[16];
+  __shared__ float red[32];
   const int b = blockIdx.x, tid = threadIdx.x;
   float np = 0.f, nn = 0.f, gi = 0.f;
   for (int l = tid; l < L; l += blockDim.x) {
@@ -56,8 +56,7 @@ __global__ __launch_bounds__(1024) void bwd_coef_kernel(
     nn += (v == 0.0f) ? 1.0f : 0.0f;
     gi = fmaxf(gi, (gI ? fabsf(gI[o]) : 0.0f) + (gIL ? fabsf(gIL[o]) : 0.0f));
   }
-  np = block_reduce<false>(np, red);
-  nn = block_reduce<false>(nn, red);
+  block_reduce2<false>(np, nn, red);
   gi = block_reduce<true>(gi, red);
   const float nrm = np * nn;
   const float gt = gscal[MPV_G_TOTAL];
@@ -67,6 +66,7 @@ __global__ __launch_bounds__(1024) void bwd_coef_kernel(
                          (live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C_X))) != 0};
   const float inv_B = 1.0f / (float)B;
   float bound = kBoundInd * gi / S_total;
+  float bmaxb[2];
 #pragma unroll
   for (int br = 0; br < 2; ++br) {
     const float M = bstat[(2 * br) * B + b], Z = bstat[(2 * br + 1) * B + b];
@@ -86,8 +86,11 @@ __global__ __launch_bounds__(1024) void bwd_coef_kernel(
       coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP;
       coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN;
     }
-    bound += block_reduce<true>(bmax, red);
+    bmaxb[br] = bmax;
   }
+  block_reduce2<true>(bmaxb[0], bmaxb[1], red);
+  bound += bmaxb[0];
+  bound += bmaxb[1];
   if (tid == 0 && gbound) gbound[b] = bound;
 }
 

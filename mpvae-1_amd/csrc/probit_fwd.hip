@@ -2033,7 +2033,7 @@ __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restri
                                                          float* __restrict__ rowstat,
                                                          float* __restrict__ bstat, int S, int B,
                                                          int L, int nNt) {
-  __shared__ float red[16];
+  __shared__ float red[32];
   const int b = blockIdx.x, tid = threadIdx.x;
   float np = 0.f, nn = 0.f;
   for (int l = tid; l < L; l += blockDim.x) {
@@ -2041,8 +2041,7 @@ __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restri
     np += (v == 1.0f) ? 1.0f : 0.0f;
     nn += (v == 0.0f) ? 1.0f : 0.0f;
   }
-  np = block_reduce<false>(np, red);
-  nn = block_reduce<false>(nn, red);
+  block_reduce2<false>(np, nn, red);
   const float nrm = np * nn;  // normalizers = |pos| * |neg|  (mpvae.py:115-117)
 
   float me = -INFINITY, mx = -INFINITY, ce = 0.f, cx = 0.f;
@@ -2063,17 +2062,14 @@ __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restri
     ce += isfinite(le) ? le : 0.0f;
     cx += isfinite(lx) ? lx : 0.0f;
   }
-  me = block_reduce<true>(me, red);
-  mx = block_reduce<true>(mx, red);
-  ce = block_reduce<false>(ce, red);
-  cx = block_reduce<false>(cx, red);
+  block_reduce2<true>(me, mx, red);
+  block_reduce2<false>(ce, cx, red);
   float ze = 0.f, zx = 0.f;
   for (int s = tid; s < S; s += blockDim.x) {
     ze += expf(rowstat[((int64_t)0 * B + b) * S + s] - me);
     zx += expf(rowstat[((int64_t)1 * B + b) * S + s] - mx);
   }
-  ze = block_reduce<false>(ze, red);
-  zx = block_reduce<false>(zx, red);
+  block_reduce2<false>(ze, zx, red);
   if (tid == 0) {
     bstat[0 * B + b] = me;
     bstat[1 * B + b] = ze;
