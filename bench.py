@@ -12,6 +12,12 @@ gradient sums (mpvae_dist.py).
 
     python bench.py [--gpus N --steps K --warmup W --config c4|c2|c3|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+``python bench.py --gpus N`` (N > 1, no WORLD_SIZE in the environment) starts
+its own N rank processes (mpvae_launch.py) before any GPU call and prints rank
+0's line.  MPVAE_DIST_BACKEND=gloo runs the exchange over gloo instead of RCCL
+and maps ranks onto the visible GPUs round robin: a rehearsal of the N-rank
+path on a one-GPU box (tests/test_gpu_dist.py), not a scaling measurement.
 """
 import argparse
 import json
@@ -27,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 import mpvae  # noqa: E402
 import mpvae_hip as H  # noqa: E402
+import mpvae_launch  # noqa: E402
 
 METRIC = "probit MC label-samples/sec (B×n_sample×L) at 1/2/4/8 GPU; ELBO rel-err"
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense f32-input MFMA (= f32 vector peak)
@@ -52,14 +59,24 @@ def log(*a):
 
 
 def setup_dist():
+    """(world, rank, cuda device index) from the launcher's environment."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MPVAE_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    if backend == "gloo":
+        local = local % max(1, n_dev)   # rehearsal: several ranks may share a GPU
+    elif local >= n_dev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {n_dev} GPUs visible")
     torch.cuda.set_device(local)
     # MPVAE_FORCE_DIST=1: a process group (and the sample-shard exchange) even
     # on one rank -- rehearses the RCCL path on a single-GPU box
     if world > 1 or os.environ.get("MPVAE_FORCE_DIST") == "1":
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -271,6 +288,11 @@ def main():
     ap.add_argument("--graph", action="store_true")
     cli = ap.parse_args()
 
+    if mpvae_launch.needs_spawn(cli.gpus):
+        # plain `python bench.py --gpus N`: N rank processes, started before
+        # this process makes any GPU call; rank 0's JSON line is relayed
+        sys.exit(mpvae_launch.launch_ranks(cli.gpus, [sys.executable, os.path.abspath(__file__)]
+                                           + sys.argv[1:]))
     world, rank, local = setup_dist()
     forced = dist.is_initialized() and world == 1
     if world != cli.gpus:
@@ -341,7 +363,9 @@ def main():
                                    f"B={B}, L={L}, z={z}, "
                                    f"n_sample={S_total} ({S_local}/GPU), philox noise on device",
                        "global_batch": B, "n_sample": S_total, "label_dim": L, "z_dim": z,
-                       "parallelism": f"n_sample-sharded x{world}", "gemm": cli.gemm},
+                       "parallelism": f"n_sample-sharded x{world}", "gemm": cli.gemm,
+                       "dist_backend": (os.environ.get("MPVAE_DIST_BACKEND", "nccl")
+                                        if dist.is_initialized() else None)},
             "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
         }
         if graph_note:

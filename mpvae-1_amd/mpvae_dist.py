@@ -29,10 +29,13 @@ silently.  Two guards:
   * the Philox seed is broadcast from the group's rank 0 (agree_seed), so a
     per-rank seed (the common seed + rank pattern) cannot split the noise;
   * verify_replicas compares an order-sensitive fp64 checksum of those four
-    tensors across ranks (all_reduce MIN and MAX) and raises ReplicaMismatch
-    on every rank when they differ.  It costs one host sync, so it runs on the
-    first sharded compute_loss of the process and then only when
-    args.mpvae_check_replicas is True (False disables it entirely).
+    tensors across ranks (all_reduce MIN and MAX of its bit pattern, so NaNs
+    and infinities in identical replicas compare equal) and raises
+    ReplicaMismatch on every rank when they differ.  It costs one host sync, so
+    by default it runs on the first sharded compute_loss of the process only;
+    args.mpvae_check_replicas = True checks every call, an int k > 1 every k-th
+    call (catches later drift, e.g. from nondeterministic MLP backward kernels),
+    False never.
 """
 import torch
 import torch.distributed as dist
@@ -42,7 +45,7 @@ class ReplicaMismatch(RuntimeError):
     """Ranks of a sample-sharded compute_loss hold different inputs."""
 
 
-_FIRST_CALL_CHECKED = False
+_SHARDED_CALLS = 0
 
 
 def replica_checksum(tensors):
@@ -87,12 +90,14 @@ class SampleShardExchange:
         tensors.  No-op unless this exchange was built with verify=True."""
         if not self.verify:
             return
-        ck = replica_checksum(tensors)
+        # compare bit patterns: a NaN checksum (NaN in a replica) or one of
+        # opposite infinities must not make identical replicas differ
+        ck = replica_checksum(tensors).view(torch.int64)
         lo, hi = ck.clone(), ck.clone()
         dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
         if not torch.equal(lo, hi):
-            bad = [i // 2 for i in range(ck.numel()) if float(lo[i]) != float(hi[i])]
+            bad = [i // 2 for i in range(ck.numel()) if int(lo[i]) != int(hi[i])]
             names = ["input_label", "fe_out", "fx_out", "r_sqrt_sigma"]
             raise ReplicaMismatch(
                 "sample-sharded compute_loss: ranks hold different "
@@ -130,8 +135,9 @@ def shard_for(args, n_sample, group=None):
     args.mpvae_force_exchange runs the collectives even on a world of one (a
     rehearsal of the multi-GPU path on a single GPU).  args.mpvae_check_replicas:
     None (default) verifies the replica contract on the first sharded call of
-    the process, True on every call, False never."""
-    global _FIRST_CALL_CHECKED
+    the process, True on every call, an int k > 1 on every k-th call, False
+    never."""
+    global _SHARDED_CALLS
     if not getattr(args, "mpvae_shard", False) or not dist.is_available() \
             or not dist.is_initialized():
         return Shard(n_sample, 0, None)
@@ -142,6 +148,11 @@ def shard_for(args, n_sample, group=None):
         raise ValueError(f"n_sample={n_sample} cannot be sharded over {world} ranks")
     S_local, s_offset = split_samples(n_sample, world, rank)
     check = getattr(args, "mpvae_check_replicas", None)
-    verify = bool(check) if check is not None else not _FIRST_CALL_CHECKED
-    _FIRST_CALL_CHECKED = True
+    if check is None:
+        verify = _SHARDED_CALLS == 0
+    elif isinstance(check, bool) or int(check) <= 1:
+        verify = bool(check)
+    else:
+        verify = _SHARDED_CALLS % int(check) == 0
+    _SHARDED_CALLS += 1
     return Shard(S_local, s_offset, SampleShardExchange(group, verify=verify))

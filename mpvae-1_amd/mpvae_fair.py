@@ -70,7 +70,17 @@ def pattern_hash(words):
 
 class LabelDistanceTable:
     """One target label's ``label_distances[target]`` dict (label string ->
-    distance) as a device open-addressing table (mpv_label_table)."""
+    distance) as a device open-addressing table (mpv_label_table).
+
+    ``ref_dtype`` is decided once per table: float64 if any value is a numpy
+    float64, else float32.  The reference decides per batch, from the values
+    actually looked up (``torch.tensor(weights)``) and promoted over the
+    targets that were active in that batch -- a data-dependent host decision.
+    The two agree whenever a table's values share one type (every
+    label_distance*.py table does); for a table mixing Python floats and numpy
+    float64, or an fp64 table inactive in a batch beside an active fp32 one,
+    the returned loss is fp64 where the reference's is fp32, a difference of
+    fp32 rounding only (the arithmetic is fp64 here either way)."""
 
     def __init__(self, distances, label_dim, device):
         self.L, self.W = label_dim, (label_dim + 63) // 64
@@ -184,7 +194,7 @@ def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, 
     norm = NORMS.get(fairness_loss_norm, 0)
     loss = _FairPenalty.apply(indiv_prob_label, indiv_prob, w, gid, order, goff, G, norm,
                               fair_coeff)
-    if all(t.ref_dtype == torch.float32 for t in tables):
+    if tables and all(t.ref_dtype == torch.float32 for t in tables):
         loss = loss.float()
     return loss, count
 

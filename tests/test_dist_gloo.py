@@ -73,6 +73,22 @@ def test_sharded_elbo_matches_unsharded_reference(world):
             assert ok, (rank, name, errs)
 
 
+def test_check_replicas_schedule(monkeypatch):
+    """mpvae_check_replicas: None -> first sharded call only, True -> every
+    call, k > 1 -> every k-th call, False -> never."""
+    import argparse
+    import mpvae_dist as D
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(D.dist, "get_world_size", lambda group=None: 2)
+    monkeypatch.setattr(D.dist, "get_rank", lambda group=None: 0)
+    for check, want in ((None, [1, 0, 0, 0, 0]), (True, [1] * 5), (False, [0] * 5),
+                        (3, [1, 0, 0, 1, 0])):
+        monkeypatch.setattr(D, "_SHARDED_CALLS", 0)
+        a = argparse.Namespace(mpvae_shard=True, mpvae_check_replicas=check)
+        got = [int(D.shard_for(a, 10).exchange.verify) for _ in range(5)]
+        assert got == want, (check, got)
+
+
 def test_split_samples_covers_axis():
     for n, w in [(10, 3), (4096, 8), (7, 7), (1000, 6)]:
         parts = [split_samples(n, w, r) for r in range(w)]
@@ -100,10 +116,12 @@ def _replica_worker(rank, world, port, q):
               "r_sqrt_sigma"]}
         noise = torch.from_numpy(f["noise"][s_off:s_off + S_local].copy())
         outcome = []
-        for perturb in (False, True):
+        for perturb in (False, True, "nan"):
             fe = t["fe_out"].clone()
-            if perturb and rank == world - 1:
+            if perturb is True and rank == world - 1:
                 fe[0, 0] += 1e-3   # one element on one rank
+            if perturb == "nan":   # identical NaN / opposite infinities on every rank
+                fe[0, 0], fe[1, 1], fe[2, 2] = float("nan"), float("inf"), float("-inf")
             cfg = ElboConfig(f.S, S_local, s_off, f.nll_coeff, f.c_coeff,
                              backend=OracleShardBackend(), exchange=ex)
             try:
@@ -131,4 +149,4 @@ def test_replica_contract_is_enforced():
         assert p.exitcode == 0
     for rank, seeds, outcome in results:
         assert seeds == (1000, 2 ** 64 - 1, 7000, (1,), "torch.int64"), (rank, seeds)
-        assert outcome == ["ok", "mismatch"], (rank, outcome)
+        assert outcome == ["ok", "mismatch", "ok"], (rank, outcome)

@@ -12,7 +12,7 @@ from mpvae_ops import ElboConfig, HipShardBackend, ProbitELBO
 from golden_io import DIFF, OUTS, PART_KEYS, fixtures
 from oracle import philox, probit_elbo as pe
 from tolerances import (EXTREME_FWD_RTOL, EXTREME_GRAD_RTOL, FWD_RTOL, GRAD_RTOL,
-                        HEADLINE_GRAD_RTOL, LONG_K_GRAD_RTOL, rel_err)
+                        HEADLINE_GRAD_RTOL, LONG_K_GRAD_RTOL, record, rel_err)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -46,8 +46,10 @@ def test_golden_forward_and_gradients(f, kind):
     noise = torch.from_numpy(f["noise"])
     out = _call(t, f.args(mpvae_noise=noise))
     ftol = EXTREME_FWD_RTOL if f.extreme else FWD_RTOL
-    for k, o in zip(OUTS, out):
-        e = rel_err(_np(o), f["out_" + k])
+    ferr = {k: rel_err(_np(o), f["out_" + k]) for k, o in zip(OUTS, out)}
+    if f.mode != "train" or kind == "gtot":
+        record(f"golden_{f.name}_fwd", ferr)
+    for k, e in ferr.items():
         assert e <= ftol, (k, e)
     if f.mode != "train":
         return
@@ -58,11 +60,15 @@ def test_golden_forward_and_gradients(f, kind):
         obj = sum(float(a) * o for a, o in zip(f["a_parts"], out[1:6]))
     obj.backward()
     gtol = EXTREME_GRAD_RTOL if f.extreme else GRAD_RTOL
+    gerr = {}
     for k, v in f.grads(kind).items():
         g = _np(t[k].grad)
         assert t[k].grad.dtype == t[k].dtype, k
         assert np.array_equal(np.isnan(g), np.isnan(v)), f"NaN pattern of d{k}"
-        assert rel_err(g, v) <= gtol, (k, rel_err(g, v))
+        gerr["d" + k] = rel_err(g, v)
+    record(f"golden_{f.name}_{kind}", gerr)
+    for k, e in gerr.items():
+        assert e <= gtol, (k, e)
 
 
 def test_default_noise_is_the_reference_cpu_draw():
@@ -255,6 +261,7 @@ def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True)
 @pytest.mark.parametrize("L,z,B,S,d", RANDOM_CASES)
 def test_random_against_oracle(L, z, B, S, d, gemm):
     ferr, gerr = _against_oracle(L, z, B, S, d, gemm, 0.5, 10.0, L * 7 + S)
+    record(f"random_{L}_{z}_{B}_{S}_{gemm}", {**ferr, **{"d" + k: v for k, v in gerr.items()}})
     for k, e in ferr.items():
         assert e <= FWD_RTOL, (k, e)
     gtol = LONG_K_GRAD_RTOL if z >= 2048 else GRAD_RTOL
@@ -272,7 +279,8 @@ def test_headline_coefficients_against_oracle(gemm, with_gI):
     total_loss alone the gradients are conditioned at ~1e-4 by the fp32 rounding
     of t (tolerances.py, HEADLINE_GRAD_RTOL)."""
     ferr, gerr = _against_oracle(1024, 1024, 64, 16, 50, gemm, 0.1, 200.0, 2024, with_gI=with_gI)
-    print(gemm, with_gI, "fwd", ferr, "grad", gerr)
+    record(f"headline_b64_{gemm}_{'with_gI' if with_gI else 'total_only'}",
+           {**ferr, **{"d" + k: v for k, v in gerr.items()}})
     for k, e in ferr.items():
         assert e <= FWD_RTOL, (k, e)
     gtol = GRAD_RTOL if with_gI else HEADLINE_GRAD_RTOL
@@ -285,19 +293,24 @@ def test_headline_batch_against_oracle():
     coefficients, total_loss as the objective (tolerances.py,
     HEADLINE_GRAD_RTOL: conditioned at ~1e-4 by the fp32 rounding of t)."""
     ferr, gerr = _against_oracle(1024, 1024, 512, 2, 50, "f16x3", 0.1, 200.0, 77, with_gI=False)
-    print("fwd", ferr, "grad", gerr)
+    record("headline_b512_s2", {**ferr, **{"d" + k: v for k, v in gerr.items()}})
     for k, e in ferr.items():
         assert e <= FWD_RTOL, (k, e)
     for k, e in gerr.items():
         assert e <= HEADLINE_GRAD_RTOL, (k, e)
 
 
-def test_shard_invariance_at_c4_size():
-    """Size-independent property at the headline size (B=512, S=4096, L=z=1024):
-    two S-shards combined exactly equal one unsharded evaluation (philox noise
-    is keyed on the global sample index)."""
-    B, S, L, z, d = 512, 4096, 1024, 1024, 50
-    g = torch.Generator(device=DEV).manual_seed(3)
+# full-size property configs: (B, S, L, z, d, first shard's samples)
+# C3 and C4 are BASELINE configs[2..3]; C5 is configs[4] at its whole
+# n_sample = 8192 on ONE GPU (about 210 GB of HBM for the backward), a superset
+# of the 1024-sample shard each of the 8 GPUs evaluates
+PROP_CFGS = {"c3": (256, 2000, 81, 81, 50, 700), "c4": (512, 4096, 1024, 1024, 50, 1536),
+             "c5": (512, 8192, 4096, 4096, 50, 3000)}
+
+
+def _prop_inputs(cfg, seed):
+    B, S, L, z, d, cut = PROP_CFGS[cfg]
+    g = torch.Generator(device=DEV).manual_seed(seed)
     y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
     y[:, 0], y[:, 1] = 1, 0
     fe = torch.randn((B, L), device=DEV, generator=g)
@@ -305,6 +318,15 @@ def test_shard_invariance_at_c4_size():
     mus = [torch.randn((B, d), device=DEV, generator=g) for _ in range(4)]
     R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
          * (6.0 / (L + z)) ** 0.5)
+    return (B, S, L, z, d, cut), y, fe, fx, mus, R
+
+
+@pytest.mark.parametrize("cfg", sorted(PROP_CFGS))
+def test_shard_invariance_full_size(cfg):
+    """Size-independent property at a BASELINE config's full size: two S-shards
+    combined exactly equal one unsharded evaluation (philox noise is keyed on
+    the global sample index)."""
+    (B, S, L, z, d, cut), y, fe, fx, mus, R = _prop_inputs(cfg, 3)
     be = HipShardBackend()
     Rop = be.prepare_R(R)
     seed = 987654321
@@ -316,31 +338,31 @@ def test_shard_invariance_at_c4_size():
 
     shape, full = local(S, 0)
     out_full = be.finalize(shape, full["bstat"], full["colsum"], *mus, 0.5, 10.0)
-    _, a = local(1536, 0)
-    _, b = local(S - 1536, 1536)
+    _, a = local(cut, 0)
+    _, b = local(S - cut, cut)
     bstat = be.combine_bstats(torch.stack([a["bstat"], b["bstat"]]))
     colsum = a["colsum"] + b["colsum"]
     out_sh = be.finalize(shape, bstat, colsum, *mus, 0.5, 10.0)
+    errs = {}
     for k, o1, o2 in zip(OUTS, out_full, out_sh):
         assert torch.isfinite(o1).all(), k
-        assert rel_err(_np(o2), _np(o1)) <= 1e-5, k
+        errs[k] = rel_err(_np(o2), _np(o1))
+    record(f"{cfg}_fwd_shard_invariance", errs)
+    for k, e in errs.items():
+        assert e <= 1e-5, (k, e)
     p = _np(out_full[6])
     assert (p > 0).all() and (p < 1).all()
 
 
-def test_backward_shard_invariance_at_c4_size():
+@pytest.mark.parametrize("cfg", sorted(PROP_CFGS))
+def test_backward_shard_invariance_full_size(cfg):
     """The backward kernels with S_local < S_total and s_offset > 0:
-    two ragged S-shards (1500 + 2596 samples) each run backward_local with the
-    combined global bstat; their packed [d fe_out | d fx_out | dR] buffers
-    summed (what the rank all_reduce does) equal the unsharded backward."""
-    B, S, L, z = 512, 4096, 1024, 1024
-    g = torch.Generator(device=DEV).manual_seed(4)
-    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
-    y[:, 0], y[:, 1] = 1, 0
-    fe = torch.randn((B, L), device=DEV, generator=g)
-    fx = torch.randn((B, L), device=DEV, generator=g)
-    R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
-         * (6.0 / (L + z)) ** 0.5)
+    two ragged S-shards each run backward_local with the combined global bstat;
+    their packed [d fe_out | d fx_out | dR] buffers summed (what the rank
+    all_reduce does) equal the unsharded backward.  The shards' statistics come
+    from a forward-only pass first, so only one shard's T is alive at a time."""
+    (B, S, L, z, d, cut), y, fe, fx, _, R = _prop_inputs(cfg, 4)
+    g = torch.Generator(device=DEV).manual_seed(40)
     g_I = torch.randn((B, L), device=DEV, generator=g)
     g_IL = torch.randn((B, L), device=DEV, generator=g)
     # g_total, g_nll, g_nll_x, g_c, g_c_x (g_kl does not reach these kernels)
@@ -350,10 +372,10 @@ def test_backward_shard_invariance_at_c4_size():
     Rop = be.prepare_R(R)
     seed = 13572468
 
-    def fwd(S_loc, s_off):
+    def fwd(S_loc, s_off, keep_T=True):
         shape = be.shape(S_loc, S, s_off, B, L, z)
         eps = be.make_noise(shape, DEV, seed, 0)
-        return shape, eps, be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=True)
+        return shape, eps, be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep_T)
 
     def bwd(shape, eps, loc, bstat):
         saved = dict(y=y, fe_out=fe, fx_out=fx, eps=eps, T=loc["T"], rowstat=loc["rowstat"],
@@ -364,39 +386,42 @@ def test_backward_shard_invariance_at_c4_size():
     shape, eps, loc = fwd(S, 0)
     full = bwd(shape, eps, loc, loc["bstat"])
     del eps, loc
-    a, b = fwd(1500, 0), fwd(S - 1500, 1500)
-    bstat = be.combine_bstats(torch.stack([a[2]["bstat"], b[2]["bstat"]]))
-    sh = bwd(*a, bstat)
-    sh += bwd(*b, bstat)
+    parts = [(cut, 0), (S - cut, cut)]
+    bstat = be.combine_bstats(torch.stack([fwd(n, o, keep_T=False)[2]["bstat"] for n, o in parts]))
+    sh = None
+    for n, o in parts:
+        part = bwd(*fwd(n, o), bstat)
+        sh = part if sh is None else sh + part
+        del part
     torch.cuda.synchronize()
     n = B * L
+    errs = {}
     for name, sl in (("d fe_out", slice(0, n)), ("d fx_out", slice(n, 2 * n)),
                      ("dR", slice(2 * n, None))):
         assert torch.isfinite(full[sl]).all(), name
-        e = rel_err(_np(sh[sl]), _np(full[sl]))
+        errs[name] = rel_err(_np(sh[sl]), _np(full[sl]))
+    record(f"{cfg}_bwd_shard_invariance", errs)
+    for name, e in errs.items():
         assert e <= 1e-5, (name, e)
 
 
-def test_full_size_train_step_is_finite_and_deterministic():
-    """C4 forward+backward with philox noise: finite, and bitwise reproducible
-    (no atomics anywhere in the kernels)."""
-    B, S, L, z, d = 512, 4096, 1024, 1024, 50
-    g = torch.Generator(device=DEV).manual_seed(5)
-    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
-    y[:, 0], y[:, 1] = 1, 0
-    base = [torch.randn((B, L), device=DEV, generator=g) for _ in range(2)]
-    mus = [torch.randn((B, d), device=DEV, generator=g) for _ in range(4)]
-    R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.03)
+@pytest.mark.parametrize("cfg", sorted(PROP_CFGS))
+def test_full_size_train_step_is_finite_and_deterministic(cfg):
+    """forward+backward at a BASELINE config's full size with philox noise:
+    finite, and bitwise reproducible (no atomics anywhere in the kernels)."""
+    (B, S, L, z, d, _), y, fe, fx, mus, R = _prop_inputs(cfg, 5)
+    R = R.detach() * (0.03 / float(R.abs().max()))
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
                               mode="train", nll_coeff=0.1, c_coeff=200.0, mpvae_noise="philox",
                               mpvae_seed=42)
     res = []
     for _ in range(2):
-        leaves = [x.clone().requires_grad_(True) for x in [base[0], mus[0], mus[1], base[1],
+        leaves = [x.clone().requires_grad_(True) for x in [fe, mus[0], mus[1], fx,
                                                             mus[2], mus[3], R]]
         out = mpvae.compute_loss(y, *leaves, args)
         out[0].backward()
-        res.append([out[0].detach().clone()] + [x.grad.clone() for x in leaves])
+        res.append([o.detach().clone() for o in out] + [x.grad.clone() for x in leaves])
+        del out, leaves
     for a, b in zip(*res):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)

@@ -74,28 +74,31 @@ def _has_finite_grad(model):  # fairsoft_utils.py:28-41
     return all(torch.isfinite(p.grad).all() for p in model.parameters() if p.grad is not None)
 
 
-def _train_steps(use_ours, steps=3):
+def _train_steps(use_ours, steps=3, feature_dim=30, label_dim=12, z_dim=12, latent_dim=8,
+                 batch=16, n_train_sample=32, nll_coeff=0.5, c_coeff=10.0, lr=1e-3):
     """The live loop body of fairsoft_train.py:45-146 (penalty-free): forward ->
     compute_loss -> backward -> clip 10 -> finite gate -> Adam step."""
-    args = _args(feature_dim=30, label_dim=12, z_dim=12, latent_dim=8, n_train_sample=32)
+    args = _args(feature_dim=feature_dim, label_dim=label_dim, z_dim=z_dim, latent_dim=latent_dim,
+                 n_train_sample=n_train_sample, nll_coeff=nll_coeff, c_coeff=c_coeff)
     model = _seeded_model(args, seed=7).to(DEV).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5)
     g = torch.Generator().manual_seed(11)
-    X = torch.randn(3 * 16, 30, generator=g)
-    Y = (torch.rand(3 * 16, 12, generator=g) < 0.3).float()
+    X = torch.randn(steps * batch, feature_dim, generator=g)
+    Y = (torch.rand(steps * batch, label_dim, generator=g) < 0.3).float()
     Y[:, 0], Y[:, 1] = 1, 0
     torch.manual_seed(5)
     torch.cuda.manual_seed(5)
     losses = []
     for i in range(steps):
         opt.zero_grad()
-        feat, label = X[16 * i:16 * (i + 1)].to(DEV), Y[16 * i:16 * (i + 1)].to(DEV)
+        sl = slice(batch * i, batch * (i + 1))
+        feat, label = X[sl].to(DEV), Y[sl].to(DEV)
         if use_ours:
             out = model(label, feat)
             res = mpvae.compute_loss(label, *out, model.r_sqrt_sigma, args)
         else:
             out = torch_ref.vae_forward_reference_order(model, label, feat)
-            noise = torch.normal(0, 1, size=(32, 16, 12)).to(DEV)   # mpvae.py:162
+            noise = torch.normal(0, 1, size=(n_train_sample, batch, z_dim)).to(DEV)  # mpvae.py:162
             res = torch_ref.elbo_naive(label, *out, model.r_sqrt_sigma, noise, args.nll_coeff,
                                        args.c_coeff)
         res[0].backward()
@@ -112,3 +115,31 @@ def test_dropin_training_loop_tracks_reference():
     np.testing.assert_allclose(l1, l2, rtol=1e-4)
     for k in p1:
         torch.testing.assert_close(p1[k], p2[k], rtol=1e-3, atol=1e-5, msg=k)
+
+
+def test_has_finite_grad_multi_tensor_path_on_device():
+    """mpvae_step.has_finite_grad on CUDA grads (the fused multi-tensor
+    _foreach_norm path training uses), mixed fp32 / fp64 gradients, against the
+    reference's per-parameter isnan / isinf answer (fairsoft_utils.py:28-41)."""
+    import mpvae_step
+    args = _args()
+    model = _seeded_model(args).to(DEV)
+    for p in model.parameters():
+        if p.requires_grad:
+            p.grad = torch.randn_like(p)
+    ref = lambda: all(not (torch.isnan(p.grad).any() or torch.isinf(p.grad).any())
+                      for p in model.parameters() if p.grad is not None)
+    assert model.r_sqrt_sigma.grad.dtype == torch.float64
+    assert mpvae_step.has_finite_grad(model) is True and ref()
+    for name, bad in (("fx1.weight", float("nan")), ("fe2.bias", float("inf")),
+                      ("r_sqrt_sigma", float("-inf")), ("r_sqrt_sigma", float("nan")),
+                      ("label_mp_mu.weight", float("-inf"))):
+        p = dict(model.named_parameters())[name]
+        keep = p.grad.clone()
+        p.grad.view(-1)[p.grad.numel() // 2] = bad
+        assert mpvae_step.has_finite_grad(model) is False and not ref(), (name, bad)
+        p.grad.copy_(keep)
+        assert mpvae_step.has_finite_grad(model) is True
+    # a huge-but-finite gradient must not overflow the reduction
+    model.fx1.weight.grad.fill_(3e38)
+    assert mpvae_step.has_finite_grad(model) is True and ref()

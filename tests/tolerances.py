@@ -40,6 +40,19 @@ EXTREME_FWD_RTOL = 1e-3
 EXTREME_GRAD_RTOL = 5e-2
 
 
+def record(test_id, errs):
+    """Append the measured errors of one parity case to
+    $MPVAE_RECORD_ERRS (a JSON-lines file) when that is set: the evidence
+    behind the tolerances above (profiles/r03_parity_errors.json)."""
+    import json
+    import os
+    path = os.environ.get("MPVAE_RECORD_ERRS")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test_id, "errs": {k: float(v) for k, v in errs.items()}})
+                    + "\n")
+
+
 def rel_err(a, b):
     import numpy as np
     a = np.asarray(a, np.float64)
