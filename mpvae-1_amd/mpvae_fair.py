@@ -131,16 +131,51 @@ def label_weights(labels, tables):
     return w, count
 
 
-def sensitive_groups(sensitive_feat):
-    """Group id per row = index of its row in torch.unique(sensitive_feat, dim=0)
-    (fairsoft_train.py:80, :103-104), rows listed group by group, offsets."""
-    _, gid = torch.unique(sensitive_feat, dim=0, return_inverse=True)
-    gid = gid.to(torch.int32)
-    G = int(gid.max().item()) + 1 if gid.numel() else 0
+def group_ids(sensitive_feat):
+    """Row b's index in ``torch.unique(sensitive_feat, dim=0)`` (the reference's
+    group order, fairsoft_train.py:80, :103-104), from fixed-size tensor ops:
+    the number of distinct rows that sort before row b (lexicographically).
+    No data-dependent shape and no host sync, so it can be captured in a HIP
+    graph; O(B^2 n_sensitive) compares, a few microseconds at B = 512."""
+    X = sensitive_feat.reshape(sensitive_feat.shape[0], -1)
+    B = X.shape[0]
+    if B == 0:
+        return torch.zeros(0, dtype=torch.int32, device=X.device)
+    ne = X[:, None, :] != X[None, :, :]                         # [c, b, j]
+    differ = ne.any(-1)                                         # rows c, b differ
+    first = ne.to(torch.uint8).argmax(-1, keepdim=True)         # first differing column
+    less = differ & (torch.gather(X[:, None, :].expand(B, B, X.shape[1]), 2, first) <
+                     torch.gather(X[None, :, :].expand(B, B, X.shape[1]), 2, first)).squeeze(-1)
+    # row c is the first occurrence of its pattern: no earlier identical row
+    earlier = torch.ones(B, B, dtype=torch.bool, device=X.device).triu(1)  # [c', c]: c' < c
+    firsts = ~((~differ) & earlier).any(0)
+    return (less & firsts[:, None]).sum(0).to(torch.int32)
+
+
+def sensitive_groups(sensitive_feat, max_groups=None):
+    """(gid, order, goff, G, overflow): group id per row (``group_ids``), the
+    rows listed group by group, and the group offsets, for G group slots.  G is
+    ``max_groups`` (an upper bound on the distinct sensitive patterns of a
+    batch, e.g. of the whole dataset, known on the host once) or the batch
+    size: the slots past the batch's own groups stay empty, and an empty group
+    adds nothing (its weight sum is 0, the reference's
+    ``weight_sensitive.sum() > 0`` gate).  A batch with more distinct patterns
+    than ``max_groups`` sets the 0-d bool device tensor ``overflow`` (its ids
+    are clamped into range, so no kernel reads out of bounds; the penalty
+    turns NaN).  Nothing here waits for the device."""
+    gid = group_ids(sensitive_feat)
+    B = gid.numel()
+    G = int(max_groups) if max_groups is not None else max(B, 1)
+    if G < 1:
+        raise ValueError(f"max_groups must be >= 1 (got {max_groups})")
+    overflow = (gid >= G).any()
+    gid = gid.clamp(max=G - 1)
     order = torch.argsort(gid, stable=True).to(torch.int32)
+    counts = torch.zeros(G, dtype=torch.int32, device=gid.device)
+    counts.index_add_(0, gid.long(), torch.ones_like(gid))
     goff = torch.zeros(G + 1, dtype=torch.int32, device=gid.device)
-    goff[1:] = torch.cumsum(torch.bincount(gid, minlength=G), 0).to(torch.int32)
-    return gid.contiguous(), order.contiguous(), goff, G
+    goff[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return gid.contiguous(), order.contiguous(), goff, G, overflow
 
 
 class _FairPenalty(torch.autograd.Function):
@@ -175,7 +210,7 @@ NORMS = {"l1": H.FAIR_L1, "l2": H.FAIR_L2}
 
 
 def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, tables,
-                     fairness_loss_norm, fair_coeff):
+                     fairness_loss_norm, fair_coeff, max_groups=None):
     """fairsoft_train.py:75-131 on the device.
 
     indiv_prob_label, indiv_prob -- compute_loss outputs 8 and 7 (label_z, feat_z)
@@ -183,6 +218,12 @@ def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, 
     sensitive_feat                -- (B, n_sensitive) (data.sensitive_feat[idx])
     tables                        -- [LabelDistanceTable(label_distances[t], L, dev)
                                       for t in target_fair_labels]
+    max_groups                    -- optional upper bound on the distinct sensitive
+                                     patterns in a batch (default: the batch size;
+                                     a batch with more distinct patterns than the
+                                     bound makes the penalty NaN)
+    No host sync: the call (forward and backward) can be captured in a HIP
+    graph (tests/test_gpu_fair.py).
     Returns ``(fairloss, contributed)``: fairloss is a differentiable 0-d
     tensor to add to total_loss (zero when no term is active), computed in fp64
     and returned in the reference's dtype (fp64 if any table holds numpy
@@ -190,10 +231,12 @@ def fairness_penalty(indiv_prob_label, indiv_prob, input_label, sensitive_feat, 
     int32 count that the reference adds to contributed_reg_fair_sample."""
     H.require_gpu(indiv_prob_label, indiv_prob, input_label, sensitive_feat)
     w, count = label_weights(input_label, tables)
-    gid, order, goff, G = sensitive_groups(sensitive_feat)
+    gid, order, goff, G, overflow = sensitive_groups(sensitive_feat, max_groups)
     norm = NORMS.get(fairness_loss_norm, 0)
     loss = _FairPenalty.apply(indiv_prob_label, indiv_prob, w, gid, order, goff, G, norm,
                               fair_coeff)
+    if max_groups is not None:  # G < B: a batch may hold more patterns than the bound
+        loss = torch.where(overflow, torch.full_like(loss, float("nan")), loss)
     if tables and all(t.ref_dtype == torch.float32 for t in tables):
         loss = loss.float()
     return loss, count

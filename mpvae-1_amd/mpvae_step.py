@@ -48,3 +48,87 @@ def step_scalars(**tensors):
         for k, v in zip(names, vals.cpu().tolist()):
             out[k] = v
     return out
+
+
+class TrainStep:
+    """The loop body of fairsoft_train.py:47-146 (penalty-free) as one call:
+    ``model(label, feat)`` -> ``compute_loss`` -> ``backward`` ->
+    ``clip_grad_norm_(10)`` -> finite-gradient gate -> optimizer step.
+
+    The gate runs on the device: the optimizer must be a fused Adam
+    (``torch.optim.Adam(..., fused=True)``), which takes ``found_inf`` and skips
+    the update on the device, step counters included -- the reference's
+    ``if has_finite_grad(model): optimizer.step()`` without the host sync.
+    ``updates`` counts the applied steps (the reference's succses_updates) on
+    the device.  With ``args.mpvae_noise = "philox"`` and a device-tensor
+    ``args.mpvae_seed`` nothing in the step waits for the host, so
+    ``capture()`` records it in one HIP graph (input batches are copied into
+    the static ``label`` / ``feat`` buffers before each ``replay()``).
+    A scheduler stepped only on applied updates (fairsoft_train.py:143-144)
+    needs the host, and stays the caller's (eager) business."""
+
+    def __init__(self, model, optimizer, args, max_grad_norm=10.0, advance_seed=True):
+        if not optimizer.defaults.get("fused"):
+            raise ValueError("TrainStep gates the update on the device: use a fused optimizer "
+                             "(torch.optim.Adam(..., fused=True))")
+        self.model, self.opt, self.args = model, optimizer, args
+        self.max_grad_norm = max_grad_norm
+        self.advance_seed = advance_seed
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        dev = self.params[0].device
+        self.updates = torch.zeros((), dtype=torch.int64, device=dev)
+        self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
+        self.graph = None
+        self.label = self.feat = self.out = None
+
+    def _body(self, label, feat):
+        import mpvae
+        self.opt.zero_grad(set_to_none=True)
+        seed = getattr(self.args, "mpvae_seed", None)
+        if self.advance_seed and isinstance(seed, torch.Tensor):
+            seed.add_(1)  # fresh probit noise every step, on the device
+        out = self.model(label, feat)
+        res = mpvae.compute_loss(label, *out, self.model.r_sqrt_sigma, self.args)
+        res[0].backward()
+        torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
+        grads = [p.grad for p in self.params if p.grad is not None]
+        peaks = torch._foreach_norm(grads, float("inf"))  # NaN-propagating max |g|
+        bad = torch.stack([~torch.isfinite(pk) for pk in peaks]).any()
+        self.found_inf.copy_(bad.to(torch.float32))
+        self.opt.found_inf = self.found_inf
+        try:
+            self.opt.step()
+        finally:
+            del self.opt.found_inf
+        self.updates.add_(1 - bad.to(torch.int64))
+        return res
+
+    def __call__(self, label, feat):
+        """One eager step; returns compute_loss's 8 outputs (device tensors)."""
+        if self.graph is not None:
+            self.label.copy_(label)
+            self.feat.copy_(feat)
+            self.graph.replay()
+            return self.out
+        return self._body(label, feat)
+
+    def capture(self, label, feat, warmup=2):
+        """Record the step in a HIP graph on static copies of (label, feat);
+        later calls copy their batch in and replay.  ``warmup`` eager steps on a
+        side stream first (they update the model, as any step does).  The
+        optimizer must be built with ``capturable=True`` (its step counter and
+        bias corrections then live on the device)."""
+        if not all(g.get("capturable") for g in self.opt.param_groups):
+            raise ValueError("capture() needs torch.optim.Adam(..., fused=True, capturable=True)")
+        self.label, self.feat = label.clone(), feat.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self._body(self.label, self.feat)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.out = self._body(self.label, self.feat)
+        return self.graph

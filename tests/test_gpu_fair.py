@@ -104,3 +104,55 @@ def test_train_metrics_training_size_against_oracle():
     res = mf.compute_metrics(torch.from_numpy(p).to(DEV), torch.from_numpy(t).to(DEV), 0.5)
     v = np.array([float(res[k]) for k in mf.METRIC_KEYS])
     assert np.allclose(v, of.train_metrics(p, t, 0.5), rtol=2e-6, atol=1e-7)
+
+
+def test_fair_penalty_is_graph_capturable():
+    """fairness_penalty forward + backward with no host sync: captured in a HIP
+    graph, replays on new batch contents equal eager calls (SURVEY 8(f) rank
+    3); a max_groups bound gives the same value as the default bound."""
+    rng = np.random.default_rng(5)
+    B, L = 256, 300
+    lab = torch.from_numpy((rng.random((B, L)) < 0.05).astype(np.float32)).to(DEV)
+    dists = [{"".join(r.astype(int).astype(str)): float(rng.uniform(0.1, 1))
+              for r in lab.cpu().numpy()[i::3]} for i in range(2)]
+    tables = [mf.LabelDistanceTable(d, L, DEV) for d in dists]
+    sens = torch.from_numpy(rng.integers(0, 3, (B, 2))).to(DEV)
+    lz = torch.from_numpy(rng.uniform(0.01, 0.99, (B, L)).astype(np.float32)).to(DEV)
+    fz = torch.from_numpy(rng.uniform(0.01, 0.99, (B, L)).astype(np.float32)).to(DEV)
+
+    def eager(lz_v, fz_v, sens_v, mg=None):
+        a, b = lz_v.clone().requires_grad_(True), fz_v.clone().requires_grad_(True)
+        loss, cnt = mf.fairness_penalty(a, b, lab, sens_v, tables, "l2", 0.7, max_groups=mg)
+        loss.backward()
+        return loss.detach(), cnt, a.grad, b.grad
+
+    a = lz.clone().requires_grad_(True)
+    b = fz.clone().requires_grad_(True)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            a.grad = b.grad = None
+            loss, cnt = mf.fairness_penalty(a, b, lab, sens, tables, "l2", 0.7)
+            loss.backward()
+    torch.cuda.current_stream().wait_stream(side)
+    a.grad = b.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        loss, cnt = mf.fairness_penalty(a, b, lab, sens, tables, "l2", 0.7)
+        loss.backward()
+    for it in range(3):
+        new_l = torch.from_numpy(rng.uniform(0.01, 0.99, (B, L)).astype(np.float32)).to(DEV)
+        new_s = torch.from_numpy(rng.integers(0, 2 + it, (B, 2))).to(DEV)
+        with torch.no_grad():
+            a.copy_(new_l)
+            sens.copy_(new_s)
+        graph.replay()
+        torch.cuda.synchronize()
+        ref = eager(new_l, fz, new_s)
+        assert torch.equal(loss, ref[0]) and int(cnt) == int(ref[1])
+        assert torch.equal(a.grad, ref[2]) and torch.equal(b.grad, ref[3])
+        bounded = eager(new_l, fz, new_s, mg=16)
+        assert abs(float(bounded[0]) - float(ref[0])) <= 1e-12 * abs(float(ref[0]))
+    # more distinct patterns than the bound: NaN, not an out-of-bounds read
+    assert torch.isnan(eager(lz, fz, sens, mg=2)[0])

@@ -75,13 +75,18 @@ def _has_finite_grad(model):  # fairsoft_utils.py:28-41
 
 
 def _train_steps(use_ours, steps=3, feature_dim=30, label_dim=12, z_dim=12, latent_dim=8,
-                 batch=16, n_train_sample=32, nll_coeff=0.5, c_coeff=10.0, lr=1e-3):
+                 batch=16, n_train_sample=32, nll_coeff=0.5, c_coeff=10.0, lr=1e-3,
+                 trainstep=False):
     """The live loop body of fairsoft_train.py:45-146 (penalty-free): forward ->
-    compute_loss -> backward -> clip 10 -> finite gate -> Adam step."""
+    compute_loss -> backward -> clip 10 -> finite gate -> Adam step.
+    trainstep: ours through mpvae_step.TrainStep (fused Adam, device gate)."""
     args = _args(feature_dim=feature_dim, label_dim=label_dim, z_dim=z_dim, latent_dim=latent_dim,
                  n_train_sample=n_train_sample, nll_coeff=nll_coeff, c_coeff=c_coeff)
     model = _seeded_model(args, seed=7).to(DEV).train()
-    opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5)
+    opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5, fused=trainstep)
+    if trainstep:
+        import mpvae_step
+        ts = mpvae_step.TrainStep(model, opt, args)
     g = torch.Generator().manual_seed(11)
     X = torch.randn(steps * batch, feature_dim, generator=g)
     Y = (torch.rand(steps * batch, label_dim, generator=g) < 0.3).float()
@@ -93,6 +98,10 @@ def _train_steps(use_ours, steps=3, feature_dim=30, label_dim=12, z_dim=12, late
         opt.zero_grad()
         sl = slice(batch * i, batch * (i + 1))
         feat, label = X[sl].to(DEV), Y[sl].to(DEV)
+        if trainstep:
+            res = ts(label, feat)
+            losses.append(float(res[0].detach()))
+            continue
         if use_ours:
             out = model(label, feat)
             res = mpvae.compute_loss(label, *out, model.r_sqrt_sigma, args)
@@ -143,3 +152,78 @@ def test_has_finite_grad_multi_tensor_path_on_device():
     # a huge-but-finite gradient must not overflow the reduction
     model.fx1.weight.grad.fill_(3e38)
     assert mpvae_step.has_finite_grad(model) is True and ref()
+
+
+def test_train_step_device_gate_tracks_reference_loop():
+    """mpvae_step.TrainStep (fused Adam skipping on a device found_inf, no host
+    sync) follows the reference loop at C1's shapes."""
+    cfg = dict(feature_dim=1000, label_dim=38, z_dim=38, latent_dim=50, batch=32,
+               n_train_sample=10, nll_coeff=0.5, c_coeff=10.0, lr=7.5e-4, steps=4)
+    l1, p1 = _train_steps(True, trainstep=True, **cfg)
+    l2, p2 = _train_steps(False, **cfg)
+    np.testing.assert_allclose(l1, l2, rtol=1e-4)
+    for k in p1:
+        torch.testing.assert_close(p1[k], p2[k], rtol=1e-3, atol=1e-5, msg=k)
+
+
+def test_train_step_skips_nonfinite_update_on_device():
+    """A degenerate label row (no positive label) makes the ranking gradient
+    NaN (mpvae.py:118): the step must leave every parameter and the Adam step
+    count untouched, like the reference's has_finite_grad gate."""
+    import mpvae_step
+    args = _args(n_train_sample=8)
+    model = _seeded_model(args).to(DEV).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    ts = mpvae_step.TrainStep(model, opt, args)
+    label = (torch.rand(5, 6, device=DEV) < 0.5).float()
+    label[:, 0], label[:, 1] = 1, 0
+    feat = torch.randn(5, 20, device=DEV)
+    ts(label, feat)
+    assert int(ts.updates) == 1
+    before = {k: v.clone() for k, v in model.state_dict().items()}
+    bad = label.clone()
+    bad[2] = 0.0
+    ts(bad, feat)
+    assert int(ts.updates) == 1 and float(ts.found_inf) == 1.0
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert all(int(s["step"]) == 1 for s in opt.state.values())
+
+
+def test_train_step_graph_replays_match_eager():
+    """The whole step (VAE forward, compute_loss, backward, clip, gate, Adam)
+    captured in one HIP graph: replays on new batches equal eager TrainStep
+    calls (reparameterisation noise switched off, dropout off, philox probit
+    noise keyed by a device seed the step advances)."""
+    import mpvae_step
+    B, F_, L = 24, 40, 10
+
+    def make():
+        a = _args(feature_dim=F_, label_dim=L, z_dim=L, latent_dim=8, keep_prob=0.0,
+                  n_train_sample=64, mpvae_noise="philox",
+                  mpvae_seed=torch.tensor([99], dtype=torch.int64, device=DEV))
+        m = _seeded_model(a, seed=3).to(DEV).train()
+        m.reparam_noise = torch.zeros_like
+        o = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5, fused=True,
+                             capturable=True)
+        return m, mpvae_step.TrainStep(m, o, a)
+
+    g = torch.Generator().manual_seed(2)
+    batches = []
+    for _ in range(4):
+        y = (torch.rand(B, L, generator=g) < 0.3).float()
+        y[:, 0], y[:, 1] = 1, 0
+        batches.append((y.to(DEV), torch.randn(B, F_, generator=g).to(DEV)))
+    mg, tg = make()
+    me, te = make()
+    tg.capture(*batches[0], warmup=1)
+    te(*batches[0])
+    for y, x in batches[1:]:
+        og = [o.clone() for o in tg(y, x)]
+        oe = te(y, x)
+        torch.cuda.synchronize()
+        for a, b in zip(og, oe):
+            torch.testing.assert_close(a, b.detach(), rtol=1e-6, atol=0)
+    for (k, a), b in zip(mg.state_dict().items(), me.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9, msg=k)
+    assert int(tg.updates) == int(te.updates) == 4
