@@ -48,158 +48,21 @@ struct FwdParams {
 #ifndef MPV_ABL
 #define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
 #endif
-#ifndef MPV_FWD_T
-#define MPV_FWD_T 1
-#endif
-#ifndef MPV_FWD_SPREAD
-#define MPV_FWD_SPREAD 0
-#endif
-#ifndef MPV_FWD_PRIO
-#define MPV_FWD_PRIO 1
-#endif
-#ifndef MPV_FWD_WIDE
-#define MPV_FWD_WIDE 1
-#endif
-// Start-phase stagger of co-resident workgroups (study): mode 1 delays blocks
-// [256, 512), mode 2 odd blocks, mode 3 blocks with (b >> 3) odd, by
-// MPV_FWD_STAG_N x s_sleep 127 (~8k cycles each) before the first DMA.
-// Which waves of the 8-wave transposed kernel issue the stage DMA: 0 all,
-// 1 waves NW/2.. (the prio-1 half), 2 waves 0..NW/2-1.  With one half issuing,
-// the other half starts its MFMAs right after the barrier.
-#ifndef MPV_FWD_DMAW
-#define MPV_FWD_DMAW 1
-#endif
-// 256 x 256 tiles (8 waves of 128 labels x 64 samples) for the wide f16x3 case
-#ifndef MPV_FWD_BIG
-#define MPV_FWD_BIG 0
-#endif
-// epilogue study knobs: priority of every wave during the epilogue (-1: keep
-// the K-loop priorities), nontemporal T stores
-#ifndef MPV_EPI_PRIO
-#define MPV_EPI_PRIO 0
-#endif
-#ifndef MPV_T_NT
-#define MPV_T_NT 0
-#endif
-#ifndef MPV_T_SC1
-#define MPV_T_SC1 0  // study: T stash with sc1 stores (lines leave the XCD's L2): +4 %, off
-#endif
-// forward with the epilogue pipelined into the next tile's K loop
-// (probit_fwd16p_kernel; study, off): parity-correct, but 18.6 ms (1 VALU
-// filler per MFMA) / 20.2 ms (2) / 29.9 ms (no interleave) against 14.5 ms:
-// two accumulator sets + fragments spill 60 VGPRs
-#ifndef MPV_FWD_P
-#define MPV_FWD_P 0
-#endif
-#ifndef MPV_FWDP_FILL
-#define MPV_FWDP_FILL 2
-#endif
-#ifndef MPV_COMBINE_T
-#define MPV_COMBINE_T 1024  // threads of fwd_combine (one block per batch row)
-#endif
-// asymmetric sample split of the 256 x 128 tile (probit_fwd16a): 16-sample
-// blocks of waves 0-3 (the waves 4-7 stream the DMA and own the rest); 4 = even
-#ifndef MPV_FWD_TSA
-#define MPV_FWD_TSA 5
-#endif
-#ifndef MPV_EPI_UNROLL
-#define MPV_EPI_UNROLL 1  // label groups per epilogue loop iteration (1: rotate by one)
-#endif
-#ifndef MPV_FWD_PF
-#define MPV_FWD_PF 0  // study: fragments prefetched one stage ahead in registers (probit_fwd16a)
-#endif
-#ifndef MPV_FWD_LOAD
-#define MPV_FWD_LOAD 0  // study: 4 loader waves stream a ring of MPV_FWD_LOAD stages (probit_fwd16L)
-#endif
-#ifndef MPV_FWD_XFER
-#define MPV_FWD_XFER 0  // rebalance the asymmetric forward's epilogue through LDS (study: +1 %)
-#endif
-#ifndef MPV_NOISE16
-#define MPV_NOISE16 0  // study: skip the eps_lo products (timing of f16-exact noise)
-#endif
-#ifndef MPV_FWD_NSTAGE
-#define MPV_FWD_NSTAGE 2  // stage ring depth of the 256 x 128 forward tile
-#endif
-#ifndef MPV_EPI_ALT
-#define MPV_EPI_ALT 1  // alternate the two SIMD partners priority per label group: -0.9 %
-#endif
-#ifndef MPV_T_SPLIT
-#define MPV_T_SPLIT 1  // T stash per label group inside the epilogue label loop: -1.5 %
-#endif
-#ifndef MPV_MFMA_PHASED
-#define MPV_MFMA_PHASED 1  // term-by-term MFMA issue (same per-accumulator order): -0.75 %
-#endif
-#ifndef MPV_EPI_SB
-#define MPV_EPI_SB 5
-#endif
-#ifndef MPV_FWD_STAG_MODE
-#define MPV_FWD_STAG_MODE 0
-#endif
-#ifndef MPV_FWD_STAG_N
-#define MPV_FWD_STAG_N 8
-#endif
-
-// In-kernel phase stamps (timing studies only, MPV_ABL & 1024): K-loop phase
-// points of blocks 0-1 for global stages 256..287, and tile epilogue bounds.
-#if (MPV_ABL & 1024)
-__device__ unsigned long long g_fwd_stamps[2][8][32][4];
-__device__ unsigned long long g_fwd_epi[2][8][8][6];
-#define FWD_STAMP(k)                                                                  \
-  do {                                                                                \
-    if (blockIdx.x < 2 && gs >= 256 && gs < 288 && (threadIdx.x & 63) == 0)           \
-      g_fwd_stamps[blockIdx.x][threadIdx.x >> 6][gs - 256][k] = __builtin_readcyclecounter(); \
-  } while (0)
-#define FWD_ESTAMP(k)                                                                 \
-  do {                                                                                \
-    if (blockIdx.x < 2 && st - t_begin >= 8 && st - t_begin < 16 && (threadIdx.x & 63) == 0) \
-      g_fwd_epi[blockIdx.x][threadIdx.x >> 6][st - t_begin - 8][k] = __builtin_readcyclecounter(); \
-  } while (0)
-#define FWD_ESTAMP2(k)                                                                \
-  do {                                                                                \
-    if (blockIdx.x < 2 && eidx >= 8 && eidx < 16 && (threadIdx.x & 63) == 0)         \
-      g_fwd_epi[blockIdx.x][threadIdx.x >> 6][eidx - 8][k] = __builtin_readcyclecounter(); \
-  } while (0)
-#else
-#define FWD_STAMP(k) \
-  do {               \
-  } while (0)
-#define FWD_ESTAMP(k) \
-  do {                \
-  } while (0)
-#define FWD_ESTAMP2(k) \
-  do {                 \
-  } while (0)
-#endif
+// Tuning constants of the product kernels (each measured; DESIGN.md section 3
+// lists the variants that lost and were removed):
+constexpr int kCombineThreads = 1024;  // fwd_combine: one block per batch row
+constexpr int kFwdWant = 2048;         // target workgroup count of the forward grid (s-chunking)
+constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
 
 // Block id -> (group g = b*nSc + sc, label tile nt).  All nNt tiles of one
 // group get ids equal mod 8 (same XCD under round-robin dispatch; speed only).
-#ifndef MPV_FWD_POL_A
-#define MPV_FWD_POL_A 0  // study: cache policy of the eps-image DMA (lds_dma16_pol)
-#endif
-#ifndef MPV_FWD_POL_B
-#define MPV_FWD_POL_B 0  // study: cache policy of the R-image DMA (nt: +7.5 %)
-#endif
-#ifndef MPV_FWD_WANT
-#define MPV_FWD_WANT 2048  // target workgroup count of the forward grid (s-chunking; 4096-16384: ±0.5 %)
-#endif
-#ifndef MPV_FWD_CFG
-#define MPV_FWD_CFG -1  // study: force the tile configuration of a 3xf16 forward with L <= 128
-#endif
-#ifndef MPV_FWD_MAP
-#define MPV_FWD_MAP 0  // study: 1 = blocks of one XCD share the label tile (R slice) instead of the row group (+5 %)
-#endif
 MPV_DEV void decode_block(int id, int G, int nNt, int& g, int& nt) {
   const int full = (G / 8) * 8 * nNt;
   if (id < full) {
     const int q = id / (8 * nNt), r = id % (8 * nNt);
-    if (MPV_FWD_MAP) {
-      nt = r % nNt;
-      g = q * 8 + r / nNt;
-      return;
-    }
     nt = r / 8;
     g = q * 8 + (r % 8);
   } else {
@@ -633,53 +496,25 @@ struct Fwd16Dma {
   }
 
   // base: wave-uniform (SGPRs); off: per-lane byte offset (inline-asm DMA, see lds_dma16)
-  template <int POL = 0>
   MPV_DEV static void piece(const char* base, uint32_t off, char* dst) {
     if (MPV_ABL & 4) return;
-    lds_dma16_pol<POL>(base, off, lds_addr(dst));
+    lds_dma16(base, off, lds_addr(dst));
   }
 
-  // Stream the next stage (if any) into stage image `dst` (PART 1: only the
-  // eps image, 2: only the R image, 0: both; the cursor advances either way).
-  template <int PART = 0>
+  // Stream the next stage (if any) into stage image `dst`.
   MPV_DEV void issue(const FwdParams& p, char* dst, int tile_end, int nK, int b) {
     if (tile >= tile_end) return;
     const int kb = kc * kRowB;  // byte offset of the K slice within a row
-    if (PART != 2) {
 #pragma unroll
-      for (int j = 0; j < JA; ++j) {
-        const int pc = wid + j * NW;
-        if (GA % NW == 0 || pc < GA) piece<MPV_FWD_POL_A>(a_base + kb, offa[j], dst + pc * 1024);
-      }
+    for (int j = 0; j < JA; ++j) {
+      const int pc = wid + j * NW;
+      if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[j], dst + pc * 1024);
     }
-    if (PART != 1) {
 #pragma unroll
-      for (int j = 0; j < JB; ++j) {
-        const int pc = wid + j * NW;
-        if (GB % NW == 0 || pc < GB) piece<MPV_FWD_POL_B>(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
-      }
+    for (int j = 0; j < JB; ++j) {
+      const int pc = wid + j * NW;
+      if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[j], dst + BM * kRowB + pc * 1024);
     }
-    ++issued;
-    if (++kc == nK) {
-      kc = 0;
-      if (++tile < tile_end) set_tile(p, b);
-    }
-  }
-
-  // The same stage split up: piece i (0 .. JA+JB-1) of the current stage, then
-  // advance() once all of them are issued (spreads the DMA over the MFMAs).
-  MPV_DEV bool active(int tile_end) const { return tile < tile_end; }
-  MPV_DEV void piece_i(int i, char* dst) {
-    const int kb = kc * kRowB;
-    if (i < JA) {
-      const int pc = wid + i * NW;
-      if (GA % NW == 0 || pc < GA) piece(a_base + kb, offa[i], dst + pc * 1024);
-    } else {
-      const int pc = wid + (i - JA) * NW;
-      if (GB % NW == 0 || pc < GB) piece(b_base + kb, offb[i - JA], dst + BM * kRowB + pc * 1024);
-    }
-  }
-  MPV_DEV void advance(const FwdParams& p, int tile_end, int nK, int b) {
     ++issued;
     if (++kc == nK) {
       kc = 0;
@@ -715,15 +550,6 @@ MPV_DEV void fwd16_read(Frag16<TM, TN>& f, const char* base, int wm, int wn, int
 // acc += hi*hi + hi*lo + lo*hi for one K stage.
 template <int TM, int TN>
 MPV_DEV void fwd16_mfma(f32x4 (&acc)[TM][TN], const Frag16<TM, TN>& f) {
-  if (MPV_ABL & 16) {
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-        acc[m][n][0] += __builtin_bit_cast(float, __builtin_shufflevector(f.ah[m], f.bl[n], 0, 8)) +
-                        __builtin_bit_cast(float, __builtin_shufflevector(f.al[m], f.bh[n], 0, 8));
-    return;
-  }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -786,7 +612,6 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
       for (int n = 0; n < TN; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int kc = 0; kc < nK; ++kc, ++gs) {
-      FWD_STAMP(0);
       // stage gs must have landed; later stages may stay in flight (loads
       // retire in order, so stores issued after them need not be waited for)
       if (NSTAGE == 2)
@@ -794,16 +619,12 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
       else
         wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * my_pieces);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      FWD_STAMP(1);
       barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-      FWD_STAMP(2);
       dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
-      FWD_STAMP(3);
       Frag16<TM, TN> f;
       fwd16_read<TM, TN, BM>(f, smem + (gs % NSTAGE) * STAGE, wm, wn, lr, coh, col);
       fwd16_mfma<TM, TN>(acc, f);
     }
-    FWD_ESTAMP(0);
     if (MPV_ABL & 1) {
       float v = 0.f;
 #pragma unroll
@@ -814,7 +635,6 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
     } else {
       fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, st * BM, nt, red, cols);
     }
-    FWD_ESTAMP(1);
   }
   fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, red);
 }
@@ -849,83 +669,38 @@ MPV_DEV void fwd16t_read(FragT<TL, TS>& f, const char* base, int wl, int sbo, in
   }
 }
 
-// MFMAs of one stage with the DMA pieces of the next stage spread between
-// them (one piece per SPREAD (label, sample) tile pairs), so the stream never
-// stalls this wave for long on a busy address unit.
-template <int TL, int TS, int NPIECE, class Dma>
-MPV_DEV void fwd16t_mfma_dma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f, Dma& dma, bool dmaon,
-                             char* dst) {
-  constexpr int SPREAD = (TL * TS) / NPIECE > 0 ? (TL * TS) / NPIECE : 1;
-#pragma unroll
-  for (int m = 0; m < TL; ++m)
-#pragma unroll
-    for (int n = 0; n < TS; ++n) {
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
-                                                         acc[m][n], 0, 0, 0);
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
-                                                         acc[m][n], 0, 0, 0);
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
-                                                         acc[m][n], 0, 0, 0);
-      const int pi = m * TS + n;
-      if (pi % SPREAD == SPREAD - 1 && pi / SPREAD < NPIECE) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (dmaon) dma.piece_i(pi / SPREAD, dst);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-}
-
+// The same products per accumulator in the same order (hi.hi, hi.lo, lo.hi),
+// issued term by term over all tiles: consecutive MFMAs see operands of one
+// kind (-0.75 % against accumulator by accumulator).
 template <int TL, int TS>
 MPV_DEV void fwd16t_mfma(f32x4 (&acc)[TL][TS], const FragT<TL, TS>& f) {
-  if (MPV_MFMA_PHASED) {
-    // the same products per accumulator in the same order (hi.hi, hi.lo,
-    // lo.hi), issued term by term over all tiles: consecutive MFMAs see
-    // operands of one kind (study: operand-toggle power)
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
-                                                           acc[m][n], 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n)
-        if (!MPV_NOISE16)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
-                                                             acc[m][n], 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
-                                                           acc[m][n], 0, 0, 0);
-    return;
-  }
 #pragma unroll
   for (int m = 0; m < TL; ++m)
 #pragma unroll
-    for (int n = 0; n < TS; ++n) {
+    for (int n = 0; n < TS; ++n)
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.eh[n]),
                                                          acc[m][n], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < TS; ++n)
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rh[m]), as_f16x8(f.el[n]),
                                                          acc[m][n], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < TS; ++n)
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.rl[m]), as_f16x8(f.eh[n]),
                                                          acc[m][n], 0, 0, 0);
-    }
 }
 
 // Packed fp32 fma with the scalar operands broadcast from one half of a
 // register pair by op_sel.  hipcc does not fold such splats of a VGPR element
 // (a per-lane label constant) into op_sel: it materialises each splat with
 // two v_mov per use, ~10 % of the epilogue's VALU instructions.
-#ifndef MPV_EPI_BC
-#define MPV_EPI_BC 1
-#endif
 // a * b[H] + c[H]
 template <int H>
 MPV_DEV f32x2 pk_fma_bc(f32x2 a, f32x2 b, f32x2 c) {
-  if (!MPV_EPI_BC) return pk_fma(a, splat2(b[H]), splat2(c[H]));
   f32x2 d;
   if (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
@@ -939,11 +714,6 @@ MPV_DEV f32x2 pk_fma_bc(f32x2 a, f32x2 b, f32x2 c) {
 // which hipcc does not insert for an asm statement's inputs)
 template <int H>
 MPV_DEV void pk_fma2_acc_bc(f32x2 p, f32x2 q, f32x2 r, f32x2& sp, f32x2& sn) {
-  if (MPV_EPI_BC != 1) {  // 2: only pk_fma_bc in asm
-    sp = pk_fma(splat2(p[H]), r, sp);
-    sn = pk_fma(splat2(q[H]), r, sn);
-    return;
-  }
   if (H == 0)
     asm("s_nop 0\n\tv_pk_fma_f32 %0, %2, %4, %0 op_sel_hi:[0,1,1]\n\t"
         "v_pk_fma_f32 %1, %3, %4, %1 op_sel_hi:[0,1,1]"
@@ -962,8 +732,7 @@ MPV_DEV void pk_fma2_acc_bc(f32x2 p, f32x2 q, f32x2 r, f32x2& sp, f32x2& sn) {
 template <int WL, int WS, int TL, int TS, int BMT = WS * TS * 16>
 MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
                                  int b, int s0, int s_own, int nt, float* red, float* cacc,
-                                 const float* cols, bool soft_any, int eidx,
-                                 bool sync_before_red = false, int sbo = -1) {
+                                 const float* cols, bool soft_any, int sbo = -1) {
   constexpr int NT = WL * WS * 64, BM = BMT, BN = WL * TL * 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wl = wid % WL, ws = wid / WL, lr = lane & 15, lg = lane >> 4;
@@ -976,38 +745,6 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   for (int m = 0; m < TL; ++m)
 #pragma unroll
     for (int n = 0; n < TS; ++n) acc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
-  // T stash first, all label groups of a sample back to back: the 4 lane rows
-  // x TL groups cover whole 128-B lines of the sample's T row (written while
-  // still combinable in L2, rather than as half lines far apart in time)
-  if (!(MPV_ABL & 2) && !MPV_T_SPLIT && p.T != nullptr) {
-    const bool vecT = true;  // t_cols rows: 16-B aligned, pad labels (t = 0) may be written
-#pragma unroll
-    for (int n = 0; n < TS; ++n) {
-      const int s = s0 + (sbo + n) * 16 + lr;
-      if (s >= s_own && s < S) {
-        float* row = p.T + ((int64_t)b * S + s) * p.ldT + n0;
-#pragma unroll
-        for (int m = 0; m < TL; ++m) {
-          const int lb = (wl * TL + m) * 16 + lg * 4;
-          const f32x4 t4 = acc[m][n];
-          if (vecT && n0 + lb < L) {
-            if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
-              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(t4)
-                           : "memory");
-            else if (MPV_T_NT)
-              __builtin_nontemporal_store(t4, reinterpret_cast<f32x4*>(row + lb));
-            else
-              *reinterpret_cast<f32x4*>(row + lb) = t4;
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (n0 + lb + i < L) row[lb + i] = t4[i];
-          }
-        }
-      }
-    }
-  }
-  FWD_ESTAMP2(1);
   // C0 x (number of this wave's samples that the column sums count)
   float ecount = 0.0f;
 #pragma unroll
@@ -1018,46 +755,34 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   ecount *= kC0;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
-  // MPV_EPI_UNROLL = U groups per (not unrolled) iteration, the accumulators
-  // rotating down by U after it: fewer register moves, U x the code
-  constexpr int EU = (MPV_EPI_UNROLL > 1 && TL % MPV_EPI_UNROLL == 0) ? MPV_EPI_UNROLL : 1;
+  // (unrolled by 2, 15 VGPRs spill; fully, 95)
 #pragma unroll 1
-  for (int mp = 0; mp < TL; mp += EU) {
-#pragma unroll
-  for (int h = 0; h < EU; ++h) {
-    const int m = mp + h;
+  for (int m = 0; m < TL; ++m) {
     f32x4 am[TS];
 #pragma unroll
-    for (int n = 0; n < TS; ++n) am[n] = acc[h][n];
-    if (h == EU - 1) {  // rotate the remaining groups down
+    for (int n = 0; n < TS; ++n) am[n] = acc[0][n];
 #pragma unroll
-      for (int mm = 0; mm + EU < TL; ++mm)
+    for (int mm = 0; mm + 1 < TL; ++mm)
 #pragma unroll
-        for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + EU][n];
-    }
+      for (int n = 0; n < TS; ++n) acc[mm][n] = acc[mm + 1][n];
     const int lb = (wl * TL + m) * 16 + lg * 4;  // first of the lane's 4 labels in the tile
-    if (MPV_EPI_ALT) {
-      // the two waves of a SIMD take turns at priority, one label group
-      // each, so that they finish the label loop together (with a fixed
-      // order one of them runs its last third alone, at half the issue rate)
-      if (((m + __builtin_amdgcn_readfirstlane(wid / (NT / 128))) & 1) != 0)
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
-    }
-    if (MPV_T_SPLIT && !(MPV_ABL & 2) && p.T != nullptr) {
-      // T stash of this label group (study: spread over the label loop)
+    // the two waves of a SIMD take turns at priority, one label group each,
+    // so that they finish the label loop together (with a fixed order one of
+    // them runs its last third alone, at half the issue rate)
+    if (((m + __builtin_amdgcn_readfirstlane(wid / (NT / 128))) & 1) != 0)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+    if (!(MPV_ABL & 2) && p.T != nullptr) {
+      // T stash of this label group, at the top of its iteration (all 16
+      // stores up front kept the prio-0 waves 4-8 K cycles in store issue)
 #pragma unroll
       for (int n = 0; n < TS; ++n) {
         const int s = s0 + (sbo + n) * 16 + lr;
         if (s >= s_own && s < S) {
           float* row = p.T + ((int64_t)b * S + s) * p.ldT + n0;
           if (n0 + lb < L) {  // t_cols rows: the pad labels' t (0) may be written
-            if (MPV_T_SC1)  // store that drops the line from L2 (keeps eps / R resident)
-              asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + lb), "v"(am[n])
-                           : "memory");
-            else
-              *reinterpret_cast<f32x4*>(row + lb) = am[n];
+            *reinterpret_cast<f32x4*>(row + lb) = am[n];
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -1097,12 +822,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       f32x2 zq[4], w4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) zq[i] = pk_fma(splat2(t4[i]), splat2(kZq), fex[i]);
-      if (MPV_ABL & 4096) {  // timing study: no probit
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w4[i] = zq[i] * 0.01f + splat2(1.0f);
-      } else {
-        probit_w2xN_zq<4>(zq, w4);
-      }
+      probit_w2xN_zq<4>(zq, w4);
       f32x2 q[4], r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1140,8 +860,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
           pk_fma2_acc_bc<0>(wpos2[i >> 1], wneg2[i >> 1], r[i], sp[n], sn[n]);
         ce[i] = pk_fma(splat2(wr), w4[i], ce[i]);  // sum E = kEh sum w + C0 count
       }
-      // MPV_EPI_SB samples at a time: bounded live ranges vs more independent chains
-      if (MPV_EPI_SB > 0 && (n + 1) % MPV_EPI_SB == 0) __builtin_amdgcn_sched_barrier(0);
+      // kEpiSampleBlocks samples at a time: bounded live ranges vs more independent chains
+      if ((n + 1) % kEpiSampleBlocks == 0) __builtin_amdgcn_sched_barrier(0);
     }
     // column sums of these 4 labels over the wave's samples: 16-lane trees
     // (8 chains step-major), lane 15 of each row accumulates into the
@@ -1163,10 +883,16 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
   }
-  }
-  FWD_ESTAMP2(2);
-  // red in a ring image: every wave must be past its last fragment read of it
-  if (sync_before_red) lds_barrier();
+  // The row sums sp / sn were last written inside pk_fma2_acc_bc's asm, which
+  // hipcc's hazard recognizer cannot see into; a VALU write must be 2 wait
+  // states ahead of the v_permlane*_swap that reads it (sum_lanegroups_n).
+  // Without this pad the swap could read the value before the last label's
+  // update, depending on how the SIMD's other wave interleaved: rowstat N
+  // was off by one e^{5E} term for 16-sample rows, run to run (found by
+  // tests/test_gpu_parity.py's full-size determinism test at C3).
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   // row statistics: sum over the 4 lane rows; lanes of row 0 publish
   float v[TS * 6];
 #pragma unroll
@@ -1186,7 +912,6 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int k = 0; k < 6; ++k) red[(wl * BM + (sbo + n) * 16 + lr) * 6 + k] = v[n * 6 + k];
   }
-  FWD_ESTAMP2(3);
   lds_barrier();
   for (int r = tid; r < BM; r += NT) {
     const int s = s0 + r;
@@ -1200,153 +925,15 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       }
     }
   }
-  FWD_ESTAMP2(4);
   lds_barrier();
 }
 
-template <int WL, int WS, int TL, int TS, int NSTAGE>
-__global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
-  constexpr int NW = WL * WS;
-  constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
-  constexpr int STAGE = (BM + BN) * kRowB;
-  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  // With a 3-deep ring the epilogue's row-sum area lives in the ring image
-  // read last (free until the next K stage refills it): the 3 stage images
-  // + column sums + label constants then fit in 160 KB.
-  constexpr bool RED_IN_RING = NSTAGE >= 3;
-  static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
-  constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + kColsT * BN) * 4];
-  float* red_own = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cacc = red_own + RED_OWN;
-  float* cols = cacc + CACC;
-
-  int g, nt;
-  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
-  const int b = g / p.nSc, sc = g % p.nSc;
-  const int n0 = nt * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = wid % WL, ws = wid / WL;
-  if (MPV_FWD_STAG_MODE) {
-    const unsigned bi = blockIdx.x;
-    const bool late = MPV_FWD_STAG_MODE == 1 ? (bi >= 256 && bi < 512)
-                      : MPV_FWD_STAG_MODE == 2 ? (bi < 512 && (bi & 1) != 0)
-                                               : (bi < 512 && ((bi >> 3) & 1) != 0);
-    if (late)
-      for (int i = 0; i < MPV_FWD_STAG_N; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-  const int lr = lane & 15, lg = lane >> 4;
-
-  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
-  const int nK = (p.z + kKC - 1) / kKC;
-  const int sw = (lr >> 1) & 7;
-  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
-  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
-
-  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
-  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
-  // does the label tile hold soft (non 0/1) labels?  (uniform; enables the
-  // two-log BCE path of the epilogue)
-  bool my_soft = false;
-  for (int i = tid; i < BN; i += NW * 64) {
-    const int l = n0 + i;
-    if (l < p.L) {
-      const float yv = p.y[(int64_t)b * p.L + l];
-      my_soft |= !(yv == 0.0f || yv == 1.0f);
-    }
-  }
-  const bool soft_any = __syncthreads_or(my_soft);
-  // DMA split (MPV_FWD_DMAW): 0 all waves, 1 the prio-1 half, 2 the other
-  // half; 3/4: the R image by waves NW/2.. before their MFMAs and the eps
-  // image by waves 0..NW/2-1 after (3) or before (4) theirs
-  constexpr bool SPLIT = MPV_FWD_DMAW >= 3;
-  constexpr int NWD = MPV_FWD_DMAW ? NW / 2 : NW;  // DMA-issuing waves (per image if SPLIT)
-  const bool dmaw = SPLIT || MPV_FWD_DMAW == 0 || ((MPV_FWD_DMAW == 1) == (wid >= NW / 2));
-  const bool rwave = wid >= NW / 2;  // SPLIT: streams the R image
-  Fwd16Dma<BM, BN, NWD> dma;
-  dma.init(p, t_begin, b, n0, (MPV_FWD_DMAW == 1 || SPLIT) ? wid % (NW / 2) : wid % NWD, lane);
-  if (dmaw) {
-#pragma unroll
-    for (int j = 0; j < NSTAGE - 1; ++j) {
-      if (!SPLIT) dma.issue(p, smem + j * STAGE, t_end, nK, b);
-      else if (rwave) dma.template issue<2>(p, smem + j * STAGE, t_end, nK, b);
-      else dma.template issue<1>(p, smem + j * STAGE, t_end, nK, b);
-    }
-  }
-
-  int gs = 0;
-  // the second half of the waves loses every age arbitration on its SIMD;
-  // static priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (MPV_FWD_PRIO && wid >= NW / 2) __builtin_amdgcn_s_setprio(MPV_FWD_PRIO);
-  for (int st = t_begin; st < t_end; ++st) {
-    const int s0 = fwd_tile_s0<BM>(st, p.S);
-    f32x4 acc[TL][TS];
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
-      FWD_STAMP(0);
-      if (NSTAGE == 2)
-        wait_vmcnt<0>();
-      else
-        wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * dma.per_wave());
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      FWD_STAMP(1);
-      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-      FWD_STAMP(2);
-      FragT<TL, TS> f;
-      if (MPV_FWD_SPREAD) {
-        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
-        const bool dmaon = dma.active(t_end);
-        fwd16t_mfma_dma<TL, TS, Fwd16Dma<BM, BN, NWD>::JA + Fwd16Dma<BM, BN, NWD>::JB>(
-            acc, f, dma, dmaon, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
-        if (dmaon) dma.advance(p, t_end, nK, b);
-      } else {
-        char* nxt = smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE;
-        if (!SPLIT) {
-          if (dmaw) dma.issue(p, nxt, t_end, nK, b);
-        } else if (rwave) {
-          dma.template issue<2>(p, nxt, t_end, nK, b);
-        } else if (MPV_FWD_DMAW == 4) {
-          dma.template issue<1>(p, nxt, t_end, nK, b);
-        }
-        FWD_STAMP(3);
-        fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
-        fwd16t_mfma<TL, TS>(acc, f);
-        if (SPLIT && MPV_FWD_DMAW == 3 && !rwave) dma.template issue<1>(p, nxt, t_end, nK, b);
-      }
-    }
-    FWD_ESTAMP(0);
-    if (MPV_ABL & 1) {  // timing study: no epilogue
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
-      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
-    } else {
-      if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
-      // ring image read by the last K stage: stages gs, gs+1 are in flight
-      float* red = RED_IN_RING
-                       ? reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE)
-                       : red_own;
-      fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                          soft_any, st - t_begin, RED_IN_RING);
-      if (MPV_EPI_PRIO >= 0) {  // back to the K-loop priorities
-        if (MPV_FWD_PRIO && wid >= NW / 2)
-          __builtin_amdgcn_s_setprio(MPV_FWD_PRIO);
-        else
-          __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    FWD_ESTAMP(5);
-  }
-  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
+// Column partials of a transposed-tile workgroup -> colpart[sc, ., b, n0 ...]
+template <int WS, int BN>
+MPV_DEV void fwd16t_colpart(const FwdParams& p, const float* cacc, int b, int sc, int n0,
+                            int nthreads) {
   lds_barrier();
-  for (int c = tid; c < BN; c += NW * 64) {
+  for (int c = threadIdx.x; c < BN; c += nthreads) {
     const int l = n0 + c;
     if (l < p.L) {
       float e = 0.f, x = 0.f;
@@ -1361,29 +948,123 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   }
 }
 
+// Does the workgroup's label tile hold soft (non 0/1) labels?  (uniform;
+// enables the two-log BCE path of the epilogue)
+template <int BN>
+MPV_DEV bool fwd_tile_soft(const FwdParams& p, int b, int n0, int nthreads) {
+  bool my_soft = false;
+  for (int i = threadIdx.x; i < BN; i += nthreads) {
+    const int l = n0 + i;
+    if (l < p.L) {
+      const float yv = p.y[(int64_t)b * p.L + l];
+      my_soft |= !(yv == 0.0f || yv == 1.0f);
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
+}
+
+// The 128 x 128 transposed tile (48 < L <= 128 on the 3xf16 path): 4 waves of
+// 64 labels x 64 samples, 2-stage ring, two workgroups per CU.  The waves of
+// the second half issue the stage DMA at static priority 1 (the other half
+// starts its MFMAs at the barrier).
+template <int WL, int WS, int TL, int TS, int NSTAGE>
+__global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
+  constexpr int NW = WL * WS;
+  constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
+  constexpr int STAGE = (BM + BN) * kRowB;
+  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN) * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL, ws = wid / WL;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  const bool soft_any = fwd_tile_soft<BN>(p, b, n0, NW * 64);
+  constexpr int NWD = NW / 2;  // DMA-issuing waves: the prio-1 half
+  const bool dmaw = wid >= NW / 2;
+  Fwd16Dma<BM, BN, NWD> dma;
+  dma.init(p, t_begin, b, n0, wid % NWD, lane);
+  if (dmaw) {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+
+  int gs = 0;
+  // the second half of the waves loses every age arbitration on its SIMD;
+  // static priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TS];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
+      if (NSTAGE == 2)
+        wait_vmcnt<0>();
+      else
+        wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * dma.per_wave());
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      FragT<TL, TS> f;
+      if (dmaw) dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
+      fwd16t_mfma<TL, TS>(acc, f);
+    }
+    if (MPV_ABL & 1) {  // timing study: no epilogue
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
+    } else {
+      __builtin_amdgcn_s_setprio(0);
+      fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                          soft_any);
+      // back to the K-loop priorities
+      if (wid >= NW / 2)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
+}
+
 // ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
 // probit_fwd16t's 256 x 128 tile with the 128 samples split unevenly between
 // the two waves of each SIMD: waves 0-3 own TSA 16-sample blocks, waves 4-7
-// TSB (< TSA) and stream every stage's DMA.  In probit_fwd16t both halves own
-// 64 samples; the DMA half then runs its 48 MFMAs after ~800 cycles of DMA
-// issue while the other half is already done and waits at the barrier.  Here
-// the DMA half has less MFMA work, so its DMA issue hides under the other
-// half's longer MFMA phase.
-// IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).  With
-// MPV_FWD_XFER the epilogue is rebalanced: A hands its last X = (TSA-TSB)/2
-// blocks to B through LDS, and each wave decodes (TSA+TSB)/2 blocks (a wave
-// alone on its SIMD issues VALU at half the SIMD's rate, so the epilogue of
-// an uneven pair lasts as long as the bigger share).
+// TSB (< TSA) and stream every stage's DMA.  With an even split the DMA half
+// runs its 48 MFMAs after ~800 cycles of DMA issue while the other half is
+// already done and waits at the barrier; here the DMA half has less MFMA
+// work, so its DMA issue hides under the other half's longer MFMA phase.
+// IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).
 template <int TSW, bool IS_A, int TSA, int TSB>
 MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cacc,
-                          const float* cols, f32x4* xfer, Fwd16Dma<128, 256, 4>& dma, bool dmaw,
-                          int b, int nt, int t_begin, int t_end, int nK, bool soft_any, int wl,
-                          int sbo, int lr, int coh, int col, float scale, bool prio1) {
-  constexpr int WL = 4, WS = 2, TL = 4, BM = 128, NSTAGE = 2;
+                          const float* cols, Fwd16Dma<128, 256, 4>& dma, bool dmaw, int b, int nt,
+                          int t_begin, int t_end, int nK, bool soft_any, int wl, int sbo, int lr,
+                          int coh, int col, float scale, bool prio1) {
+  constexpr int WL = 4, TL = 4, BM = 128, NSTAGE = 2;
   constexpr int STAGE = (BM + 256) * kRowB;
-  constexpr int X = MPV_FWD_XFER ? (TSA - TSB) / 2 : 0;
-  constexpr int TSE = X ? (TSA + TSB) / 2 : TSW;  // blocks this wave's epilogue decodes
-  const int lane = threadIdx.x & 63;
   int gs = 0;
   for (int st = t_begin; st < t_end; ++st) {
     const int s0 = fwd_tile_s0<BM>(st, p.S);
@@ -1392,44 +1073,16 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
     for (int m = 0; m < TL; ++m)
 #pragma unroll
       for (int n = 0; n < TSW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (MPV_FWD_PF) {
-      // fragments one stage ahead in registers: the MFMAs of stage gs start
-      // right after the barrier while stage gs+1's fragments are read.
-      // Stage g sits in slot g % 2 and is issued two stages ahead (at the
-      // barrier of g-2, into the slot whose fragments are already held).
-      FragT<TL, TSW> f0, f1;
-      // stage gs landed before the previous stage's barrier (or the prologue's)
-      fwd16t_read<WL, TL, TSW, BM>(f0, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
-      auto step = [&](FragT<TL, TSW>& cur, FragT<TL, TSW>& nxt, bool pf) {
-        wait_vmcnt<0>();  // DMA waves: stage gs+1 landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // cur is in registers
-        barrier_raw();
-        if (dmaw)
-          dma.issue(p, smem + (__builtin_amdgcn_readfirstlane(gs) % NSTAGE) * STAGE, t_end, nK, b);
-        if (pf)
-          fwd16t_read<WL, TL, TSW, BM>(nxt, smem + ((gs + 1) % NSTAGE) * STAGE, wl, sbo, lr, coh,
-                                       col);
-        fwd16t_mfma<TL, TSW>(acc, cur);
-        ++gs;
-      };
-      int kc = 0;
-      for (; kc + 1 < nK; kc += 2) {
-        step(f0, f1, true);
-        step(f1, f0, kc + 2 < nK);
-      }
-      if (kc < nK) step(f0, f1, false);
-    } else {
-      for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
-        wait_vmcnt<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-        if (dmaw)
-          dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
-                    t_end, nK, b);
-        FragT<TL, TSW> f;
-        fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
-        fwd16t_mfma<TL, TSW>(acc, f);
-      }
+    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      if (dmaw)
+        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
+                  t_end, nK, b);
+      FragT<TL, TSW> f;
+      fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+      fwd16t_mfma<TL, TSW>(acc, f);
     }
     if (MPV_ABL & 1) {  // timing study: no epilogue
       float v = 0.f;
@@ -1440,43 +1093,13 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
       p.rowpart[(int64_t)blockIdx.x * 512 + threadIdx.x] = v;
       continue;
     }
-    if (MPV_EPI_PRIO >= 0) __builtin_amdgcn_s_setprio(MPV_EPI_PRIO);
-    if (X > 0) {
-      // hand-off of A's last X sample blocks (t of 64 labels x 16 samples each)
-      if (IS_A) {
-#pragma unroll
-        for (int j = 0; j < X; ++j)
-#pragma unroll
-          for (int m = 0; m < TL; ++m)
-            xfer[((wl * X + j) * TL + m) * 64 + lane] = acc[m][TSW - X + j];
-      }
-      lds_barrier();
-      f32x4 e[TL][TSE];
-#pragma unroll
-      for (int m = 0; m < TL; ++m) {
-        if (IS_A) {
-#pragma unroll
-          for (int n = 0; n < TSE; ++n) e[m][n] = acc[m][n];
-        } else {
-#pragma unroll
-          for (int j = 0; j < X; ++j) e[m][j] = xfer[((wl * X + j) * TL + m) * 64 + lane];
-#pragma unroll
-          for (int n = 0; n < TSW; ++n) e[m][X + n] = acc[m][n];
-        }
-      }
-      fwd_tile_epilogue_t<WL, WS, TL, TSE, BM>(p, e, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                               soft_any, st - t_begin, false,
-                                               IS_A ? 0 : TSA - X);
-    } else {
-      fwd_tile_epilogue_t<WL, WS, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                               soft_any, st - t_begin, false, sbo);
-    }
-    if (MPV_EPI_PRIO >= 0) {
-      if (prio1)
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
-    }
+    __builtin_amdgcn_s_setprio(0);
+    fwd_tile_epilogue_t<WL, 2, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                            soft_any, sbo);
+    if (prio1)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
   }
   if (MPV_ABL & 8) wait_vmcnt<0>();  // timing study: no stage DMA left in flight at exit
 }
@@ -1488,14 +1111,10 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   static_assert(BM == 128, "the sample tile stays 128");
   constexpr int STAGE = (BM + BN) * kRowB;
   constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  constexpr int X = MPV_FWD_XFER ? (TSA - TSB) / 2 : 0;
-  static_assert(!MPV_FWD_XFER || (TSA - TSB) % 2 == 0, "even hand-off");
-  constexpr int XF = WL * X * 4 * 64 * 4;  // floats of the hand-off area
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN + XF) * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN) * 4];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red + RED;
   float* cols = cacc + CACC;
-  f32x4* xfer = reinterpret_cast<f32x4*>(cols + kColsT * BN);
 
   int g, nt;
   decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
@@ -1513,518 +1132,25 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
 
   fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
   for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
-  bool my_soft = false;
-  for (int i = tid; i < BN; i += NW * 64) {
-    const int l = n0 + i;
-    if (l < p.L) {
-      const float yv = p.y[(int64_t)b * p.L + l];
-      my_soft |= !(yv == 0.0f || yv == 1.0f);
-    }
-  }
-  const bool soft_any = __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
+  const bool soft_any = fwd_tile_soft<BN>(p, b, n0, NW * 64);
   const bool dmaw = wid >= NW / 2;  // the TSB half streams the stages
   Fwd16Dma<BM, BN, NW / 2> dma;
   dma.init(p, t_begin, b, n0, wid % (NW / 2), lane);
   if (dmaw) {
 #pragma unroll
-    for (int j = 0; j < (MPV_FWD_PF ? NSTAGE : NSTAGE - 1); ++j)
-      dma.issue(p, smem + j * STAGE, t_end, nK, b);
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
   }
-  if (MPV_FWD_PF) {  // stage 0 (and 1) landed before the first tile's fragment read
-    wait_vmcnt<0>();
-    barrier_raw();
-  }
-  const bool prio1 = MPV_FWD_PRIO && dmaw;
+  // the second half of the waves loses every age arbitration on its SIMD;
+  // static priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  const bool prio1 = dmaw;
   if (prio1) __builtin_amdgcn_s_setprio(1);
   if (wid < NW / 2)
-    fwd16a_tiles<TSA, true, TSA, TSB>(p, smem, red, cacc, cols, xfer, dma, false, b, nt, t_begin,
-                                      t_end, nK, soft_any, wl, 0, lr, coh, col, scale, prio1);
+    fwd16a_tiles<TSA, true, TSA, TSB>(p, smem, red, cacc, cols, dma, false, b, nt, t_begin, t_end,
+                                      nK, soft_any, wl, 0, lr, coh, col, scale, prio1);
   else
-    fwd16a_tiles<TSB, false, TSA, TSB>(p, smem, red, cacc, cols, xfer, dma, true, b, nt, t_begin,
-                                       t_end, nK, soft_any, wl, TSA, lr, coh, col, scale, prio1);
-  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
-  lds_barrier();
-  for (int c = tid; c < BN; c += NW * 64) {
-    const int l = n0 + c;
-    if (l < p.L) {
-      float e = 0.f, x = 0.f;
-#pragma unroll
-      for (int w = 0; w < WS; ++w) {
-        e += cacc[(w * BN + c) * 2 + 0];
-        x += cacc[(w * BN + c) * 2 + 1];
-      }
-      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + l] = e;
-      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + l] = x;
-    }
-  }
-}
-
-// ------------------------- 3xf16 with loader waves (probit_fwd16L, study)
-// probit_fwd16t's 256 x 128 tile (8 compute waves of 64 x 64) plus 4 loader
-// waves that only stream the stage images: the DMA issue (48 LDS-DMA pieces
-// per stage, ~100+ cycles each) leaves the compute waves' MFMA chain, and a
-// ring of NSTAGE images lets the loaders run NSTAGE-1 stages ahead (with 3,
-// the epilogue's row-sum area lives in the image the tile's last stage read).
-// The loaders mirror every barrier of the compute waves: one per K stage and
-// three in each tile's epilogue.  12 waves = 3 per SIMD caps the kernel at
-// 168 VGPRs.
-constexpr int kFwdLoaders = 4;
-
-template <int NSTAGE>
-MPV_DEV void fwd16L_compute(const FwdParams& p, char* smem, float* red_own, float* cacc,
-                            const float* cols, int b, int nt, int t_begin, int t_end, int nK,
-                            bool soft_any, int wl, int sbo, int lr, int coh, int col,
-                            float scale) {
-  constexpr int WL = 4, WS = 2, TL = 4, TS = 4, BM = 128;
-  constexpr int STAGE = (BM + 256) * kRowB;
-  constexpr bool RED_IN_RING = NSTAGE >= 3;
-  int gs = 0;
-  for (int st = t_begin; st < t_end; ++st) {
-    const int s0 = fwd_tile_s0<BM>(st, p.S);
-    f32x4 acc[TL][TS];
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < nK; ++kc, ++gs) {
-      // no vmcnt wait: this wave's only vector-memory ops are its T / row stores
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier_raw();  // stage gs landed (loaders waited); every wave is done reading gs-1
-      FragT<TL, TS> f;
-      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
-      fwd16t_mfma<TL, TS>(acc, f);
-    }
-    if (MPV_ABL & 1) {  // timing study: no epilogue (the loaders' barriers still matched)
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
-      p.rowpart[(int64_t)blockIdx.x * 512 + threadIdx.x] = v;
-      if (RED_IN_RING) barrier_raw();
-      barrier_raw();
-      barrier_raw();
-      continue;
-    }
-    float* red = RED_IN_RING
-                     ? reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE)
-                     : red_own;
-    fwd_tile_epilogue_t<WL, WS, TL, TS, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                             soft_any, st - t_begin, RED_IN_RING, sbo);
-  }
-}
-
-template <int NSTAGE>
-__global__ __launch_bounds__(768, 1) void probit_fwd16L_kernel(FwdParams p) {
-  constexpr int WL = 4, WS = 2, NC = 8, NW = NC + kFwdLoaders;
-  constexpr int BM = 128, BN = 256;
-  constexpr int STAGE = (BM + BN) * kRowB;
-  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  constexpr bool RED_IN_RING = NSTAGE >= 3;
-  static_assert(!RED_IN_RING || RED * 4 <= STAGE, "row-sum area must fit one stage image");
-  constexpr int RED_OWN = RED_IN_RING ? 0 : RED;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED_OWN + CACC + kColsT * BN) * 4];
-  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cacc = red + RED_OWN;
-  float* cols = cacc + CACC;
-
-  int g, nt;
-  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
-  const int b = g / p.nSc, sc = g % p.nSc;
-  const int n0 = nt * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = wid % WL;
-  const int lr = lane & 15, lg = lane >> 4;
-  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
-  const int nK = (p.z + kKC - 1) / kKC;
-  const int sw = (lr >> 1) & 7;
-  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
-  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
-
-  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
-  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
-  bool my_soft = false;
-  for (int i = tid; i < BN; i += NW * 64) {
-    const int l = n0 + i;
-    if (l < p.L) {
-      const float yv = p.y[(int64_t)b * p.L + l];
-      my_soft |= !(yv == 0.0f || yv == 1.0f);
-    }
-  }
-  const bool soft_any = __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
-  if (wid >= NC) {
-    using Dma = Fwd16Dma<BM, BN, kFwdLoaders>;
-    static_assert(Dma::EVEN, "every loader streams the same piece count");
-    constexpr int PW = Dma::JA + Dma::JB;  // pieces per loader wave per stage
-    Dma dma;
-    dma.init(p, t_begin, b, n0, wid - NC, lane);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
-    int gs = 0;
-    for (int st = t_begin; st < t_end; ++st) {
-      for (int kc = 0; kc < nK; ++kc, ++gs) {
-        // stage gs landed: leave the younger issued stages in flight
-        if (NSTAGE >= 3 && dma.issued >= gs + 2)
-          wait_vmcnt<(NSTAGE >= 3 ? PW : 0)>();
-        else
-          wait_vmcnt<0>();
-        barrier_raw();
-        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
-                  t_end, nK, b);
-      }
-      // the epilogue's barriers: red-in-ring hand-over, then the row statistics
-      if (RED_IN_RING) barrier_raw();
-      barrier_raw();
-      barrier_raw();
-    }
-  } else {
-    fwd16L_compute<NSTAGE>(p, smem, red, cacc, cols, b, nt, t_begin, t_end, nK, soft_any, wl,
-                           (wid / WL) * 4, lr, coh, col, scale);
-  }
-  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
-  lds_barrier();
-  for (int c = tid; c < BN; c += NW * 64) {
-    const int l = n0 + c;
-    if (l < p.L) {
-      float e = 0.f, x = 0.f;
-#pragma unroll
-      for (int w = 0; w < WS; ++w) {
-        e += cacc[(w * BN + c) * 2 + 0];
-        x += cacc[(w * BN + c) * 2 + 1];
-      }
-      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * p.L + l] = e;
-      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * p.L + l] = x;
-    }
-  }
-}
-
-// --------------------- 3xf16, epilogue pipelined into the next tile (fwd16p)
-// probit_fwd16t with the epilogue of tile i run INSIDE the K loop of tile
-// i+1, by the same waves: in probit_fwd16t every wave reaches the epilogue
-// together and the matrix pipe idles for about a third of each tile.  Each
-// wave keeps the previous tile's 64 accumulators (pacc) beside the current
-// ones; the K loop's first 32 stages each carry one "unit" of the previous
-// tile's epilogue -- one sample group n (16 samples, the lane's sample lr)
-// x 2 of the lane's 4 labels of label group mg -- and the scheduler is told
-// to interleave its VALU with the stage's 48 MFMAs (sched_group_barrier:
-// one MFMA, then up to two VALU).  Row statistics go out per sample group
-// into an LDS accumulator (ds_add), column sums per label group; one extra
-// barrier per tile publishes the row statistics.  The last tile's epilogue
-// runs after the loop without MFMAs.  Needs nK >= 32 (z > 992): 32 units per
-// tile; L % 4 == 0.  Same arithmetic as probit_fwd16t, other summation
-// order of the row sums (deterministic).
-namespace fwdp {
-constexpr int WL = 4, WS = 2, TL = 4, TS = 4, NW = 8, NSTAGE = 2;
-constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // 128 samples, 256 labels
-constexpr int STAGE = (BM + BN) * kRowB;             // 48 KB
-constexpr int RED = WL * BM * 6, CACC = WS * BN * 2, COLS = BN * 8;  // floats
-}  // namespace fwdp
-
-// Per-label constants of the label tile, 8 floats per label:
-// fe, fx, qa, qb, sg (ranking exponent in log2 units), wpos, wneg, y.
-MPV_DEV void fwdp_cols_stage(float* cols, const FwdParams& p, int b, int n0) {
-  for (int i = threadIdx.x; i < fwdp::BN; i += fwdp::NW * 64) {
-    const int l = n0 + i;
-    const bool ok = l < p.L;
-    const int64_t o = (int64_t)b * p.L + (ok ? l : 0);
-    const float y = ok ? p.y[o] : 0.0f;
-    const bool hard = ok && (y == 0.0f || y == 1.0f);
-    float* c = cols + i * 8;
-    c[0] = ok ? p.fe[o] : 0.0f;
-    c[1] = ok ? p.fx[o] : 0.0f;
-    c[2] = !hard ? 0.0f : (y == 0.0f ? -1.0f : 1.0f);  // q = qa E + qb
-    c[3] = !hard ? 1.0f : (y == 0.0f ? 1.0f : 0.0f);
-    c[4] = y == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
-    c[5] = (ok && y == 1.0f) ? 1.0f : 0.0f;
-    c[6] = (ok && y == 0.0f) ? 1.0f : 0.0f;
-    c[7] = ok ? y : 0.0f;
-  }
-}
-
-// Unit (n, h) of the previous tile for label group mg: labels lb+2h, lb+2h+1.
-template <int H, bool SOFT>
-MPV_DEV void fwdp_unit(const f32x4& t4, const float* cols, int lb, float wr, f32x2& sl,
-                       f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
-  const f32x4 ca = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H) * 8);
-  const f32x4 cb = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H) * 8 + 4);
-  const f32x4 da = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H + 1) * 8);
-  const f32x4 db = *reinterpret_cast<const f32x4*>(cols + (lb + 2 * H + 1) * 8 + 4);
-  const f32x2 u[2] = {splat2(t4[2 * H]) + f32x2{ca[0], ca[1]},
-                      splat2(t4[2 * H + 1]) + f32x2{da[0], da[1]}};
-  f32x2 E[2];
-  probit_prob2xN<2>(u, E);
-  const f32x2 q0 = pk_fma(E[0], splat2(ca[2]), splat2(ca[3]));
-  const f32x2 q1 = pk_fma(E[1], splat2(da[2]), splat2(da[3]));
-  const f32x2 a0 = E[0] * cb[0], a1 = E[1] * db[0];
-  const f32x2 r0 = f32x2{__builtin_amdgcn_exp2f(a0.x), __builtin_amdgcn_exp2f(a0.y)};
-  const f32x2 r1 = f32x2{__builtin_amdgcn_exp2f(a1.x), __builtin_amdgcn_exp2f(a1.y)};
-  const f32x2 q = q0 * q1;  // >= (4.7e-7)^2: one log for both labels
-  f32x2 lp = f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)};
-  if (SOFT) {  // a soft label adds both BCE terms (its q is 1); branch-free
-    const float y0 = cb[3], y1 = db[3];
-    // weight 1 for a soft label (qa = 0, y != 0; pad labels have y = 0), else 0
-    const float w0 = (ca[2] == 0.0f && y0 != 0.0f) ? 1.0f : 0.0f;
-    const float w1 = (da[2] == 0.0f && y1 != 0.0f) ? 1.0f : 0.0f;
-    const f32x2 o0 = splat2(1.0f) - E[0], o1 = splat2(1.0f) - E[1];
-    lp += splat2(w0) * f32x2{y0 * __builtin_amdgcn_logf(E[0].x) + (1.0f - y0) * __builtin_amdgcn_logf(o0.x),
-                             y0 * __builtin_amdgcn_logf(E[0].y) + (1.0f - y0) * __builtin_amdgcn_logf(o0.y)};
-    lp += splat2(w1) * f32x2{y1 * __builtin_amdgcn_logf(E[1].x) + (1.0f - y1) * __builtin_amdgcn_logf(o1.x),
-                             y1 * __builtin_amdgcn_logf(E[1].y) + (1.0f - y1) * __builtin_amdgcn_logf(o1.y)};
-  }
-  sl = sl + lp;
-  sp = pk_fma(splat2(cb[1]), r0, pk_fma(splat2(db[1]), r1, sp));
-  sn = pk_fma(splat2(cb[2]), r0, pk_fma(splat2(db[2]), r1, sn));
-  ce[2 * H] = pk_fma(splat2(wr), E[0], ce[2 * H]);
-  ce[2 * H + 1] = pk_fma(splat2(wr), E[1], ce[2 * H + 1]);
-}
-
-// Stage reads + MFMAs of one K stage (fragments of R per label group just in
-// time), optionally with one epilogue unit interleaved.
-template <bool UNIT, int H, bool SOFT>
-MPV_DEV void fwdp_stage(f32x4 (&acc)[fwdp::TL][fwdp::TS], const char* base, int wl, int ws, int lr,
-                        int coh, int col, const f32x4& t4, const float* cols, int lb, float wr,
-                        f32x2& sl, f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
-  using namespace fwdp;
-  FragT<TL, TS> f;
-  fwd16t_read<WL, TL, TS, BM>(f, base, wl, ws * TS, lr, coh, col);
-  if (UNIT) fwdp_unit<H, SOFT>(t4, cols, lb, wr, sl, sp, sn, ce);
-  fwd16t_mfma<TL, TS>(acc, f);
-  if (UNIT && MPV_FWDP_FILL > 0) {
-    // interleave: the unit's VALU between the stage's MFMAs
-#pragma unroll
-    for (int i = 0; i < 48; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, MPV_FWDP_FILL, 0);  // VALU fillers
-    }
-  }
-}
-
-// Row statistics of sample group n (both halves done): reduce over the 4 lane
-// rows and accumulate into red (this wave owns these entries: plain LDS adds).
-MPV_DEV void fwdp_rowstats(float* red, int wl, int ws, int n, int lr, int lg, f32x2& sl, f32x2& sp,
-                           f32x2& sn) {
-  using namespace fwdp;
-  sl = sl * 0.6931471805599453f;
-  const float v[6] = {sl.x, sl.y, sp.x, sn.x, sp.y, sn.y};
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const float tot = sum_lanegroups(v[k]);
-    if (lg == 0) atomicAdd(red + (wl * BM + (ws * TS + n) * 16 + lr) * 6 + k, tot);
-  }
-  sl = sp = sn = splat2(0.0f);
-}
-
-// the kernel's LDS (file scope, so that both instantiations of fwdp_main
-// address it as LDS directly)
-__shared__ __attribute__((aligned(1024))) char fwdp_smem[fwdp::NSTAGE * fwdp::STAGE +
-                                                         (fwdp::RED + fwdp::CACC + fwdp::COLS) * 4];
-
-template <bool SOFT>
-MPV_DEV void fwdp_main(const FwdParams& p) {
-  using namespace fwdp;
-  char* smem = fwdp_smem;
-  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cacc = red + RED;
-  float* cols = cacc + CACC;
-  int g, nt;
-  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
-  const int b = g / p.nSc, sc = g % p.nSc;
-  const int n0 = nt * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = wid % WL, ws = wid / WL;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.S, L = p.L;
-  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
-  const int nK = (p.z + kKC - 1) / kKC;  // >= 32 (host check)
-  const int sw = (lr >> 1) & 7;
-  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
-  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
-  constexpr int NWD = NW / 2;  // the prio-1 half issues the stage DMA
-  const bool dmaw = wid >= NW / 2;
-  Fwd16Dma<BM, BN, NWD> dma;
-  dma.init(p, t_begin, b, n0, wid - NW / 2, lane);
-  if (dmaw) {
-#pragma unroll
-    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
-  }
-  if (dmaw) __builtin_amdgcn_s_setprio(1);
-
-  f32x4 acc[TL][TS], pacc[TL][TS];
-  int gs = 0;
-  int prev_s0 = 0, prev_own = 0;
-  f32x2 sl = splat2(0.f), sp = splat2(0.f), sn = splat2(0.f);
-  f32x2 ce[4];
-
-  // one K stage: wait for its DMA, barrier, stream the next stage
-#define stage_head()                                                                      \
-  do {                                                                                    \
-    wait_vmcnt<0>();                                                                      \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                    \
-    barrier_raw(); /* stage gs landed for every wave; every wave is done reading gs-1 */  \
-    if (dmaw) dma.issue(p, fwdp_smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) %   \
-                                        NSTAGE) * STAGE, t_end, nK, b);                       \
-  } while (0)
-  // after the 8 units of label group mg: column sums into cacc, rotate pacc
-  auto group_tail = [&](int mg) {
-    const int lb = (wl * TL + mg) * 16 + lg * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float e = row16_sum_to_lane15(ce[i].x), x = row16_sum_to_lane15(ce[i].y);
-      if (lr == 15) {
-        float* c = cacc + (ws * BN + lb + i) * 2;
-        c[0] += e;
-        c[1] += x;
-      }
-      ce[i] = splat2(0.0f);
-    }
-#pragma unroll
-    for (int mm = 0; mm + 1 < TL; ++mm)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) pacc[mm][n] = pacc[mm + 1][n];
-  };
-  // the previous tile's row statistics: red -> rowpart (one extra barrier)
-  auto publish_rows = [&]() {
-    lds_barrier();
-    for (int r = tid; r < BM; r += NW * 64) {
-      const int s = prev_s0 + r;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        float v = 0.0f;
-#pragma unroll
-        for (int w = 0; w < WL; ++w) {
-          v += red[(w * BM + r) * 6 + k];
-          red[(w * BM + r) * 6 + k] = 0.0f;
-        }
-        if (s >= prev_own && s < S) p.rowpart[(((int64_t)k * p.nNt + nt) * p.B + b) * S + s] = v;
-      }
-    }
-  };
-  // unit j (0..7) of label group mg of the previous tile: sample group n = j/2, half j%2
-#define FWDP_UNIT_ARGS(J)                                                                   \
-  pacc[0][(J) / 2], cols, (wl * TL + mg) * 16 + lg * 4,                                     \
-      (prev_s0 + (ws * TS + (J) / 2) * 16 + lr >= prev_own &&                                 \
-       prev_s0 + (ws * TS + (J) / 2) * 16 + lr < S) ? 1.0f : 0.0f,                            \
-      sl, sp, sn, ce
-  // T stash of sample group n of the previous tile (16 B per lane, 4 labels)
-  auto store_t = [&](int mg, const f32x4& t4, int n) {
-    const int s = prev_s0 + (ws * TS + n) * 16 + lr;
-    const int lb = (wl * TL + mg) * 16 + lg * 4;
-    if (s >= prev_own && s < S && n0 + lb < L)
-      *reinterpret_cast<f32x4*>(p.T + ((int64_t)b * S + s) * p.ldT + n0 + lb) = t4;
-  };
-
-  bool have_prev = false;
-  for (int st = t_begin; st <= t_end; ++st) {
-    const bool mf = st < t_end;  // uniform
-    const int s0 = mf ? fwd_tile_s0<BM>(st, S) : 0;
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ce[i] = splat2(0.0f);
-    if (mf && have_prev) {
-      for (int mg = 0; mg < TL; ++mg) {
-#define FWDP_STEP(J)                                                                          \
-  do {                                                                                        \
-    stage_head();                                                                             \
-    if ((J) % 2 == 0) store_t(mg, pacc[0][(J) / 2], (J) / 2);                                  \
-    fwdp_stage<true, (J) % 2, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col,         \
-                              FWDP_UNIT_ARGS(J));                                             \
-    if ((J) % 2 == 1) fwdp_rowstats(red, wl, ws, (J) / 2, lr, lg, sl, sp, sn);                  \
-    ++gs;                                                                                     \
-  } while (0)
-        FWDP_STEP(0); FWDP_STEP(1); FWDP_STEP(2); FWDP_STEP(3);
-        FWDP_STEP(4); FWDP_STEP(5); FWDP_STEP(6); FWDP_STEP(7);
-#undef FWDP_STEP
-        group_tail(mg);
-      }
-      for (int kc = 32; kc < nK; ++kc, ++gs) {
-        stage_head();
-        fwdp_stage<false, 0, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col, acc[0][0],
-                             cols, 0, 0.0f, sl, sp, sn, ce);
-      }
-      publish_rows();
-    } else if (mf) {  // first tile: nothing to overlap
-      for (int kc = 0; kc < nK; ++kc, ++gs) {
-        stage_head();
-        fwdp_stage<false, 0, SOFT>(acc, smem + (gs % NSTAGE) * STAGE, wl, ws, lr, coh, col, acc[0][0],
-                             cols, 0, 0.0f, sl, sp, sn, ce);
-      }
-    } else if (have_prev) {  // drain: the last tile's epilogue alone
-      for (int mg = 0; mg < TL; ++mg) {
-#define FWDP_DRAIN(J)                                                                         \
-  do {                                                                                        \
-    if ((J) % 2 == 0) store_t(mg, pacc[0][(J) / 2], (J) / 2);                                  \
-    fwdp_unit<(J) % 2, SOFT>(FWDP_UNIT_ARGS(J));                                                    \
-    if ((J) % 2 == 1) fwdp_rowstats(red, wl, ws, (J) / 2, lr, lg, sl, sp, sn);                  \
-  } while (0)
-        FWDP_DRAIN(0); FWDP_DRAIN(1); FWDP_DRAIN(2); FWDP_DRAIN(3);
-        FWDP_DRAIN(4); FWDP_DRAIN(5); FWDP_DRAIN(6); FWDP_DRAIN(7);
-#undef FWDP_DRAIN
-        group_tail(mg);
-      }
-      publish_rows();
-    }
-    if (mf) {
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TS; ++n) pacc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
-      prev_s0 = s0;
-      prev_own = st * BM;
-    }
-    have_prev = mf;
-  }
-#undef FWDP_UNIT_ARGS
-#undef stage_head
-  // column partials of this workgroup -> colpart[sc, ., b, n0 ...]
-  lds_barrier();
-  for (int c = tid; c < BN; c += NW * 64) {
-    const int l = n0 + c;
-    if (l < L) {
-      float e = 0.f, x = 0.f;
-#pragma unroll
-      for (int w = 0; w < WS; ++w) {
-        e += cacc[(w * BN + c) * 2 + 0];
-        x += cacc[(w * BN + c) * 2 + 1];
-      }
-      p.colpart[(((int64_t)sc * 2 + 0) * p.B + b) * L + l] = e;
-      p.colpart[(((int64_t)sc * 2 + 1) * p.B + b) * L + l] = x;
-    }
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void probit_fwd16p_kernel(FwdParams p) {
-  using namespace fwdp;
-  char* smem = fwdp_smem;
-  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cacc = red + RED;
-  float* cols = cacc + CACC;
-  int g, nt;
-  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
-  const int b = g / p.nSc;
-  const int n0 = nt * BN;
-  const int tid = threadIdx.x;
-  fwdp_cols_stage(cols, p, b, n0);
-  for (int i = tid; i < CACC + RED; i += NW * 64) red[i] = 0.0f;  // red, cacc adjacent
-  bool my_soft = false;
-  for (int i = tid; i < BN; i += NW * 64) {
-    const int l = n0 + i;
-    if (l < p.L) {
-      const float yv = p.y[(int64_t)b * p.L + l];
-      my_soft |= !(yv == 0.0f || yv == 1.0f);
-    }
-  }
-  // readfirstlane: the compiler must see the branch (around the whole main
-  // loop) as uniform, or every value inside turns divergent
-  if (__builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)))  // two-log BCE terms
-    fwdp_main<true>(p);
-  else
-    fwdp_main<false>(p);
+    fwd16a_tiles<TSB, false, TSA, TSB>(p, smem, red, cacc, cols, dma, true, b, nt, t_begin, t_end,
+                                       nK, soft_any, wl, TSA, lr, coh, col, scale, prio1);
+  fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
@@ -2138,18 +1264,19 @@ struct FwdPlan {
 
 static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
-  const bool wide = MPV_FWD_WIDE && gemm == MPV_GEMM_F16X3 && s->L > 128;
-  // 3xf16 with 48 < L <= 96: the 128 x 128 transposed tile beats the 96-label
-  // one in spite of its pad labels (C3, L = 81: forward 0.216 -> 0.167 ms)
+  // tile configurations: 0 = 48 labels (L <= 48), 1 = 96 labels (fp32 mode,
+  // L <= 96), 2 = 128 labels (transposed 3xf16 tile, or the fp32 64 x 64
+  // waves), 3 = 256 labels (3xf16, L > 128).  3xf16 with 48 < L <= 96 takes
+  // the 128 x 128 transposed tile in spite of its pad labels (C3, L = 81:
+  // forward 0.216 -> 0.167 ms against a 96-label tile)
   const bool f16 = gemm == MPV_GEMM_F16X3;
-  pl.cfg = s->L <= 48 ? 0 : ((s->L <= 96 && !f16) ? 1 : (wide ? 3 : 2));
-  if (MPV_FWD_CFG >= 0 && f16 && s->L <= 128) pl.cfg = MPV_FWD_CFG;
-  pl.BM = (pl.cfg == 3 && MPV_FWD_BIG) ? 256 : 128;
+  pl.cfg = s->L <= 48 ? 0 : ((s->L <= 96 && !f16) ? 1 : ((f16 && s->L > 128) ? 3 : 2));
+  pl.BM = 128;
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
   // enough workgroups to fill 256 CUs several times; fewer s-chunks = fewer partials
-  int64_t want = cdiv(MPV_FWD_WANT, s->B * (int64_t)pl.nNt);
+  int64_t want = cdiv(kFwdWant, s->B * (int64_t)pl.nNt);
   if (want < 1) want = 1;
   if (want > pl.nSt) want = pl.nSt;
   pl.tps = (int)cdiv(pl.nSt, want);
@@ -2177,31 +1304,11 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 0:  // BN 48, 4 waves, 3-stage ring (66 KB LDS: 2 workgroups per CU)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 3>), grid, dim3(256), 0, st, p);
         break;
-      case 1:  // BN 96, 8 waves, 4-stage ring (112 KB); study only (MPV_FWD_CFG=1)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 2, 2, 3, 4>), grid, dim3(512), 0, st, p);
-        break;
-      case 3:  // 256 labels x 128 samples, 8 waves of 64 x 64, one workgroup per CU
-        if (MPV_FWD_BIG)  // 256 labels x 256 samples, 8 waves of 128 x 64
-          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 8, 4, 2>), grid, dim3(512), 0, st, p);
-        else
-          if (MPV_FWD_LOAD)
-            MPV_LAUNCH("probit_fwd", (probit_fwd16L_kernel<MPV_FWD_LOAD ? MPV_FWD_LOAD : 2>), grid, dim3(768), 0, st, p);
-          else if (MPV_FWD_TSA != 4 || MPV_FWD_PF)
-            MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<MPV_FWD_TSA, 8 - MPV_FWD_TSA>), grid,
-                       dim3(512), 0, st, p);
-          else
-            MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 4, 4, MPV_FWD_NSTAGE>), grid,
-                       dim3(512), 0, st, p);
+      case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
+        MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3>), grid, dim3(512), 0, st, p);
         break;
       default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
-        if (MPV_FWD_T) {
-          MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
-          break;
-        }
-        // 128 x 128 tile, 4 waves of 64 x 64 (3 MFMAs per 1.33 fragment
-                // reads), 2-stage ring (64 KB): 2 workgroups per CU, so one
-                // workgroup's epilogue (VALU) overlaps the other's MFMA phase
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
+        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
         break;
     }
   }
@@ -2223,15 +1330,6 @@ static int check_split_operand(const mpv_split16& o, int64_t rows, int64_t ld_mi
 using namespace mpv;
 
 extern "C" {
-
-#if (MPV_ABL & 1024)
-int mpv_dbg_fwd_stamps(void* host_out, void* host_epi) {
-  return (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fwd_stamps), sizeof(g_fwd_stamps)) ==
-                  hipSuccess &&
-          hipMemcpyFromSymbol(host_epi, HIP_SYMBOL(g_fwd_epi), sizeof(g_fwd_epi)) == hipSuccess)
-             ? 0 : 1;
-}
-#endif
 
 size_t mpv_fwd_workspace_bytes(const mpv_shape* shape) {
   if (check_shape(shape) != MPV_OK) return 0;
@@ -2290,15 +1388,9 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   p.nSt = pl.nSt;
   const int64_t blocks = (int64_t)shape->B * pl.nSc * pl.nNt;
   MPV_REQUIRE(blocks < (int64_t(1) << 31), "grid too large");
-  const bool pipelined = MPV_FWD_P && a->gemm == MPV_GEMM_F16X3 && pl.cfg == 3 &&
-                         pl.BM == fwdp::BM && pl.BN == fwdp::BN && cdiv(shape->z, kKC) >= 32 &&
-                         shape->L % 4 == 0 && a->T != nullptr;
-  if (pipelined)
-    MPV_LAUNCH("probit_fwd", probit_fwd16p_kernel, dim3((unsigned)blocks), dim3(512), 0, st, p);
-  else
-    launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
+  launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
-  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(MPV_COMBINE_T), 0, st, a->y,
+  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(kCombineThreads), 0, st, a->y,
              p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
   if (int rc = check_launch("fwd_combine")) return rc;
   if (pl.nSc > 1) {

@@ -427,6 +427,37 @@ def test_full_size_train_step_is_finite_and_deterministic(cfg):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,S,L,z", [(64, 777, 100, 90), (256, 2000, 81, 81), (128, 1000, 38, 38),
+                                     (64, 4096, 1024, 1024), (8, 700, 300, 200)],
+                         ids=["l100", "c3", "c2", "c4dims", "l300"])
+def test_forward_statistics_bitwise_repeatable(B, S, L, z):
+    """Every forward tile kernel (48-, 128- and 256-label tiles) gives the same
+    row statistics, batch statistics and column sums, bit for bit, over 8
+    launches.  Round 3 found the 128-label transposed kernel dropping one
+    label's e^{5E} from a 16-sample row of N now and then (timing-dependent);
+    this catches any such lost update."""
+    g = torch.Generator(device=DEV).manual_seed(L + S)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.05
+    be = HipShardBackend()
+    shape = be.shape(S, S, 0, B, L, z)
+    Rop = be.prepare_R(R)
+    eps = be.make_noise(shape, DEV, 4242, 0)
+    first = None
+    for _ in range(8):
+        loc = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=True)
+        got = [loc[k].clone() for k in ("rowstat", "bstat", "colsum")]
+        if first is None:
+            first = got
+            continue
+        for name, a, b in zip(("rowstat", "bstat", "colsum"), got, first):
+            bad = int((a != b).sum())
+            assert bad == 0, (name, bad)
+
+
 def test_gemm_modes_agree_at_c4_dims():
     """3xf16 split GEMMs vs exact fp32 MFMA on the same philox noise, at the
     headline L=z=1024, n_sample=4096 (batch 64 to keep the test short)."""
