@@ -451,19 +451,11 @@ MPV_DEV uint32_t lds_addr(const void* p) {
 // images of a ring apart), which exposes the whole DMA latency at every stage.
 // Callers order it themselves: counted s_waitcnt vmcnt + a barrier before a
 // stage is read, and a barrier after its last read before it is refilled.
-#ifndef MPV_DMA_NT
-#define MPV_DMA_NT 0  // study: nontemporal policy on the operand stream (fwd +6.5 %, dR +8 %, off)
-#endif
-#if MPV_DMA_NT
-#define MPV_DMA_POL " nt"
-#else
-#define MPV_DMA_POL ""
-#endif
 MPV_DEV void lds_dma16(const void* saddr, uint32_t voff, uint32_t lds) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2" MPV_DMA_POL "\n\ts_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(saddr), "s"(lds)
       : "memory");
@@ -473,30 +465,6 @@ MPV_DEV void lds_dma16(const void* saddr, uint32_t voff, uint32_t lds) {
 // 4, so every row starts 16-B aligned and the element pass reads whole float4
 // (ABI v5; include/mpvae_hip.h).
 __host__ __device__ inline int64_t t_cols(int64_t L) { return (L + 3) & ~int64_t(3); }
-
-// lds_dma16 with a cache policy on the load (study): POL bits 1 sc0, 2 sc1, 4 nt.
-template <int POL>
-MPV_DEV void lds_dma16_pol(const void* saddr, uint32_t voff, uint32_t lds) {
-  if constexpr (POL == 0) {
-    lds_dma16(saddr, voff, lds);
-  } else {
-    uint32_t keep;
-#define MPV_DMA_ASM_POL(MOD)                                              \
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"        \
-               "global_load_lds_dwordx4 %1, %2" MOD "\n\ts_mov_b32 m0, %0" \
-               : "=&s"(keep)                                              \
-               : "v"(voff), "s"(saddr), "s"(lds)                          \
-               : "memory")
-    if constexpr (POL == 1) MPV_DMA_ASM_POL(" sc0");
-    else if constexpr (POL == 2) MPV_DMA_ASM_POL(" sc1");
-    else if constexpr (POL == 3) MPV_DMA_ASM_POL(" sc0 sc1");
-    else if constexpr (POL == 4) MPV_DMA_ASM_POL(" nt");
-    else if constexpr (POL == 5) MPV_DMA_ASM_POL(" sc0 nt");
-    else if constexpr (POL == 6) MPV_DMA_ASM_POL(" sc1 nt");
-    else MPV_DMA_ASM_POL(" sc0 sc1 nt");
-#undef MPV_DMA_ASM_POL
-  }
-}
 
 // s_waitcnt vmcnt(n) for a wave-uniform n (the immediate must be a constant).
 MPV_DEV void wait_vmcnt_dyn(int n) {

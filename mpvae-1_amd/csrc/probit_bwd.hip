@@ -23,9 +23,6 @@
 #ifndef MPV_ABL
 #define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
 #endif
-#ifndef MPV_ELEM_NT
-#define MPV_ELEM_NT 3  // nontemporal 1: T loads, 2: G-plane stores (both: element pass -5 %)
-#endif
 
 namespace mpv {
 
@@ -184,9 +181,8 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   r.bN = f32x2{p.coef[2 * BS + cb], p.coef[5 * BS + cb]};
   const float* row = p.T + cb * p.ldT;
   if (VEC && c0 < p.L) {  // t_cols rows: the pad columns are readable
-    const f32x4 v = (MPV_ELEM_NT & 1)
-                        ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0))
-                        : *reinterpret_cast<const f32x4*>(row + c0);
+    // nontemporal T loads and G-plane stores: element pass -5 %
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + c0));
     r.t[0] = v[0]; r.t[1] = v[1]; r.t[2] = v[2]; r.t[3] = v[3];
   } else {
 #pragma unroll
@@ -194,24 +190,16 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   }
 }
 
-// Rows of T in flight per thread beyond the one computing (MPV_ELEM_LA), and
-// ONE: a block row covers all its columns (RPI == 1), so the row index and the
-// six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
-#ifndef MPV_ELEM_LA
-#define MPV_ELEM_LA 1
-#endif
-#ifndef MPV_ELEM_ST16
-#define MPV_ELEM_ST16 0  // study: G planes as 16-B stores through a DPP swap of lane pairs (+3.5 %, off)
-#endif
-#ifndef MPV_ELEM_MINR
-#define MPV_ELEM_MINR 16  // minimum T rows per thread of the element pass (C2 -6 %; 0: no minimum)
-#endif
-#ifndef MPV_ELEM_WPS
-#define MPV_ELEM_WPS 4  // minimum waves per SIMD the element pass is compiled for (128 VGPRs)
-#endif
+// Rows of T in flight per thread beyond the one computing (kElemLookahead),
+// and ONE: a block row covers all its columns (RPI == 1), so the row index and
+// the six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
+// Otherwise (L < 1024: C2, C3) they are per-lane, 12 more VGPRs than fit in
+// 128: those instantiations run at 3 waves per SIMD instead of spilling.
+constexpr int kElemLookahead = 1;
+constexpr int kElemMinRows = 16;  // minimum T rows per thread (C2 -6 %)
 template <bool VEC, bool PLANES, bool ONE>
-__global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams p) {
-  constexpr int LA = MPV_ELEM_LA;
+__global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p) {
+  constexpr int LA = kElemLookahead;
   __shared__ float cred[256 * 8];
   const int b = blockIdx.x, sc = blockIdx.y;
   const int tid = threadIdx.x;
@@ -286,34 +274,8 @@ __global__ __launch_bounds__(256, MPV_ELEM_WPS) void bwd_elem_kernel(ElemParams 
         const int64_t o = chunked_index(cb, p.gld, c0);
         const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
         const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
-        if (MPV_ELEM_ST16) {
-          // lanes 2i, 2i+1 hold columns c0, c0 + 4 of one 8-column run (TPR is
-          // a multiple of 32 on the planes path): one DPP swap hands the even
-          // lane the odd lane's hi words and the odd lane the even lane's lo,
-          // so each stores 16 B (the run's 8 hi or 8 lo halves) instead of 2 x 8
-          const bool odd = (cq & 1) != 0;
-          const uint32_t hw0 = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
-          const uint32_t hw1 = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
-          const uint32_t lw0 = (uint32_t)l[0] | ((uint32_t)l[1] << 16);
-          const uint32_t lw1 = (uint32_t)l[2] | ((uint32_t)l[3] << 16);
-          const uint32_t r0 = (uint32_t)__builtin_amdgcn_update_dpp(
-              0, (int)(odd ? hw0 : lw0), 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-          const uint32_t r1 = (uint32_t)__builtin_amdgcn_update_dpp(
-              0, (int)(odd ? hw1 : lw1), 0xB1, 0xF, 0xF, false);
-          typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
-          const u32v4 v = odd ? u32v4{r0, r1, lw0, lw1} : u32v4{hw0, hw1, r0, r1};
-          const int64_t o8 = chunked_index(cb, p.gld, c0 & ~7) + (odd ? kLoOff : 0);
-          if (MPV_ELEM_NT & 2)
-            __builtin_nontemporal_store(v, reinterpret_cast<u32v4*>(p.g + o8));
-          else
-            *reinterpret_cast<u32v4*>(p.g + o8) = v;
-        } else if (MPV_ELEM_NT & 2) {
-          __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
-          __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
-        } else {
-          *reinterpret_cast<s16x4*>(p.g + o) = hv;
-          *reinterpret_cast<s16x4*>(p.g + o + kLoOff) = lv;
-        }
+        __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
+        __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
       } else {
         float* row = p.T + cb * p.ldT;
         if (VEC && c0 < L) {  // pad columns get G = 0
@@ -375,38 +337,9 @@ struct Dr16Params {
   int nLt, nZt, nKc, rows_per_chunk, rows_pad;
 };
 
-// In-kernel phase stamps (timing studies only, MPV_ABL & 1024): s_memtime at
-// the loop's phase points of blocks 0-1, iterations 256..287, every wave.
-#if (MPV_ABL & 1024)
-__device__ unsigned long long g_dr_stamps[2][8][32][4];
-#define MPV_STAMP(k)                                                                     \
-  do {                                                                                   \
-    if (blockIdx.x < 2 && ci >= 256 && ci < 288 && (threadIdx.x & 63) == 0)              \
-      g_dr_stamps[blockIdx.x][threadIdx.x >> 6][ci - 256][k] = __builtin_readcyclecounter(); \
-  } while (0)
-#else
-#define MPV_STAMP(k) \
-  do {               \
-  } while (0)
-#endif
-#ifndef MPV_DR_UNROLL2
-#define MPV_DR_UNROLL2 0
-#endif
-#ifndef MPV_DR_KIND
-#define MPV_DR_KIND 1  // 0: 16x16x32 ring, 1: 16x16x32 staggered, 2: 32x32x16 4-deep ring, 3: 2 staggered
-#endif
-#ifndef MPV_DMA_ASM
-#define MPV_DMA_ASM 1
-#endif
-
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
-  if (MPV_ABL & 256) {
-    s16x4 v = s16x4{(short)off, 1, 2, 3};
-    asm volatile("" : "+v"(v));
-    return v;
-  }
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) s16x4*)(base + off));
 }
@@ -447,13 +380,7 @@ MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
       src = p.eps16.data + (int64_t)qb * p.eps16.ld;
       off += (min(q + lrow, rows - 1) - qb) * (int)p.eps16.ld * 2;
     }
-    if (MPV_ABL & 128) continue;
-    if (MPV_DMA_ASM)
-      lds_dma16(src, (uint32_t)off, lds_addr(dst + pc * 1024));
-    else
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + off,
-                                       (__attribute__((address_space(3))) void*)(dst + pc * 1024),
-                                       16, 0, 0);
+    lds_dma16(src, (uint32_t)off, lds_addr(dst + pc * 1024));
   }
 }
 
@@ -510,19 +437,15 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
   for (int j = 0; j < P && j < nst; ++j)
     dr_issue<PER_WAVE, PIECES, RPP>(p, smem + j * STAGE, q_begin + j * kDrKR, rows, wid, dma_off);
   for (int ci = 0; ci < nst; ++ci) {
-    MPV_STAMP(0);
     if (P == 1)
       wait_vmcnt<0>();
     else
       wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    MPV_STAMP(1);
     barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
-    MPV_STAMP(2);
     if (ci + P < nst)
       dr_issue<PER_WAVE, PIECES, RPP>(p, smem + ((ci + P) % kDrStages) * STAGE,
                                  q_begin + (ci + P) * kDrKR, rows, wid, dma_off);
-    MPV_STAMP(3);
     const char* base = smem + (ci % kDrStages) * STAGE;
     s16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
@@ -547,11 +470,6 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
     for (int m = 0; m < TM; ++m)
 #pragma unroll
       for (int n = 0; n < TN; ++n) {
-        if (MPV_ABL & 512) {
-          acc[m][n][0] += __builtin_bit_cast(float, __builtin_shufflevector(ah[m], bl[n], 0, 8)) +
-                          __builtin_bit_cast(float, __builtin_shufflevector(al[m], bh[n], 0, 8));
-          continue;
-        }
         acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bh[n]),
                                                            acc[m][n], 0, 0, 0);
         acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(ah[m]), as_f16x8(bl[n]),
@@ -603,44 +521,16 @@ MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0
   }
 }
 
-#ifndef MPV_MFMA_PHASED
-#define MPV_MFMA_PHASED 0
-#endif
-#ifndef MPV_NOISE16
-#define MPV_NOISE16 0  // study: skip the eps_lo products (timing of f16-exact noise)
-#endif
 template <int TM, int TN>
 MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
-  if (MPV_MFMA_PHASED) {  // term by term over all tiles, same order per accumulator
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
-                                                           acc[m][n], 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-    return;
-  }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
     for (int n = 0; n < TN; ++n) {
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
                                                          acc[m][n], 0, 0, 0);
-      if (!MPV_NOISE16)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
-                                                           acc[m][n], 0, 0, 0);
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
+                                                         acc[m][n], 0, 0, 0);
       acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
                                                          acc[m][n], 0, 0, 0);
     }
@@ -656,12 +546,11 @@ MPV_DEV void drs_issue_range(const Dr16Params& p, char* dst, int q0, int rows, i
     const int pc = pc0 + i;  // wave-uniform
     const bool is_g = pc < PIECES / 2;
     const int r = is_g ? pc : pc - PIECES / 2;
-    const int q = (MPV_ABL & 2048) ? ((q0 & 63) + r) : q0 + r;  // 2048: L2-resident rows (timing study)
+    const int q = q0 + r;
     const char* src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
                            : reinterpret_cast<const char*>(p.eps16.data +
                                                            (int64_t)min(q, rows - 1) * p.eps16.ld +
                                                            2 * z0);
-    if (MPV_ABL & 128) continue;
     lds_dma16(src, (uint32_t)(((lane_u ^ (r & 7)) << 5) + lane_h), lds_addr(dst + pc * 1024));
   }
 }
@@ -672,12 +561,6 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
                        int lane_u, int lane_h) {
   drs_issue_range<PER_WAVE, PIECES>(p, dst, q0, rows, wn * PER_WAVE, l0, z0, lane_u, lane_h);
 }
-
-// MPV_DR_G1P: DMA pieces per stage streamed by each group-1 wave (at the start
-// of its MFMA slot, two stages ahead), the rest by group 0 as before.
-#ifndef MPV_DR_G1P
-#define MPV_DR_G1P 0
-#endif
 
 // Staggered schedule: the waves of row wm = 0 (group 0) and wm = 1 (group 1)
 // share the SIMDs pairwise and run one phase apart, so on every SIMD one wave
@@ -699,9 +582,8 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   constexpr int STAGE = 2 * IMG;
   constexpr int PIECES = STAGE / 1024;  // 1-KB wave-instructions per stage
   constexpr int RPP = 1024 / ROWB;      // rows per piece
-  constexpr int G1P = MPV_DR_G1P;                 // pieces per group-1 wave
-  constexpr int PER_WAVE = (PIECES - WN * G1P) / WN;  // pieces per group-0 wave
-  static_assert(PIECES % WN == 0 && G1P <= PIECES / WN, "DMA pieces must split over the waves");
+  constexpr int PER_WAVE = PIECES / WN;  // pieces per group-0 wave (group 1 issues none)
+  static_assert(PIECES % WN == 0, "DMA pieces must split over the waves");
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   int kc, tile;
@@ -737,80 +619,40 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   barrier_raw();
   DrFrag<TM, TN> f;
   // the two groups run the same number of barriers: 2*nst + 1
-  // MPV_DR_UNROLL2 (study, off): two stages per iteration, so that each
-  // stage image's LDS base is a compile-time offset and the fragment reads
-  // need no per-read address arithmetic (78 VALU per 96 MFMAs today).  The
-  // hoisted addresses do not fit beside 128 accumulator + 96 fragment VGPRs:
-  // 84 VGPRs spill.
+  // (two stages per iteration, so that each image's LDS base is a constant
+  // offset, spilled 84 VGPRs: 128 accumulator + 96 fragment VGPRs leave no room
+  // for the hoisted addresses)
 #define DR_G0_STAGE(i, PAR)                                                                   \
   do {                                                                                        \
-    const int ci = (i);                                                                       \
-    (void)ci;                                                                                 \
-    MPV_STAMP(0);                                                                             \
     if ((i) + 1 < nst)                                                                        \
       drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
                                   rows, wn, l0, z0, lane_u, lane_h);                          \
-    MPV_STAMP(1);                                                                             \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
     lds_barrier();                                                                            \
-    MPV_STAMP(2);                                                                             \
     __builtin_amdgcn_s_setprio(1);                                                            \
     dr_mfma<TM, TN>(acc, f);                                                                  \
     __builtin_amdgcn_s_setprio(0);                                                            \
     wait_vmcnt<0>();                                                                          \
-    MPV_STAMP(3);                                                                             \
     barrier_raw();                                                                            \
   } while (0)
-#define DR_G1_STAGE(i, PAR)                                                        \
-  do {                                                                             \
-    const int ci = (i);                                                            \
-    (void)ci;                                                                      \
-    MPV_STAMP(0);                                                                  \
-    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);   \
-    MPV_STAMP(1);                                                                  \
-    if (G1P) wait_vmcnt<0>(); /* own share of stage (i)+1 landed */                \
-    lds_barrier();                                                                 \
-    MPV_STAMP(2);                                                                  \
-    if (G1P && (i) + 2 < nst) /* stage (i)+2 -> image PAR, read by all by now */   \
-      drs_issue_range<G1P, PIECES>(p, smem + (PAR) * STAGE, q_begin + ((i) + 2) * kDrKR, \
-                                   rows, WN * PER_WAVE + wn * G1P, l0, z0, lane_u, lane_h); \
-    __builtin_amdgcn_s_setprio(1);                                                 \
-    dr_mfma<TM, TN>(acc, f);                                                       \
-    __builtin_amdgcn_s_setprio(0);                                                 \
-    MPV_STAMP(3);                                                                  \
-    barrier_raw();                                                                 \
+#define DR_G1_STAGE(i, PAR)                                                      \
+  do {                                                                           \
+    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp); \
+    lds_barrier();                                                               \
+    __builtin_amdgcn_s_setprio(1);                                               \
+    dr_mfma<TM, TN>(acc, f);                                                     \
+    __builtin_amdgcn_s_setprio(0);                                               \
+    barrier_raw();                                                               \
   } while (0)
   if (grp == 0) {
     // slot 2i: stream stage i+1, read stage i; slot 2i+1: MFMAs of stage i
     // (stage i+1 landed before its barrier)
-    if (MPV_DR_UNROLL2) {
-      int i = 0;
-      for (; i + 1 < nst; i += 2) {
-        DR_G0_STAGE(i, 0);
-        DR_G0_STAGE(i + 1, 1);
-      }
-      if (i < nst) DR_G0_STAGE(i, 0);
-    } else {
-      for (int i = 0; i < nst; ++i) DR_G0_STAGE(i, i & 1);
-    }
+    for (int i = 0; i < nst; ++i) DR_G0_STAGE(i, i & 1);
     barrier_raw();
   } else {
-    // slot 0: group 1's share of stage 1 (image 1 is untouched so far)
-    if (G1P && nst > 1)
-      drs_issue_range<G1P, PIECES>(p, smem + STAGE, q_begin + kDrKR, rows, WN * PER_WAVE + wn * G1P,
-                                   l0, z0, lane_u, lane_h);
     barrier_raw();
     // slot 2i+1: read stage i; slot 2i+2: MFMAs of stage i
-    if (MPV_DR_UNROLL2) {
-      int i = 0;
-      for (; i + 1 < nst; i += 2) {
-        DR_G1_STAGE(i, 0);
-        DR_G1_STAGE(i + 1, 1);
-      }
-      if (i < nst) DR_G1_STAGE(i, 0);
-    } else {
-      for (int i = 0; i < nst; ++i) DR_G1_STAGE(i, i & 1);
-    }
+    for (int i = 0; i < nst; ++i) DR_G1_STAGE(i, i & 1);
   }
 #undef DR_G0_STAGE
 #undef DR_G1_STAGE
@@ -824,244 +666,6 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
         const int l = l0 + (wm * TM + m) * 16 + lg * 4 + i;
         const int zc = z0 + (wn * TN + n) * 16 + lr;
         if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][i] * inv;
-      }
-}
-
-// ---- dR on v_mfma_f32_32x32x16_f16: 16-row stages, 4-deep ring -------------
-// K = 16 per MFMA, so a stage of 16 sample rows (32 KB for a 256 x 256 tile)
-// is consumed on its own and the 128-KB ring keeps 3 stages in flight (the
-// 16x16x32 kernel above, at 32 rows per stage, fits one).  Fragment of a
-// 32-column block for lane l: column l%32, K rows 8*(l/32) .. +7, as two
-// transposed reads (rows 8*(l/32) + 4h + 0..3); A and B share that K order, so
-// it is the identity.  Image rows are 1 KB (256 columns chunked hi/lo); the
-// 32-B unit U of row r sits at U ^ ((r & 3) << 1), conflict-free for these
-// reads (checked exhaustively).
-constexpr int kDr32KR = 16;  // K rows per stage
-constexpr int kDr32NS = 4;   // ring depth
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-MPV_DEV int dr32_swz(int r) { return (r & 3) << 1; }
-
-template <int PER_WAVE, int PIECES>
-MPV_DEV void dr32_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid, int l0, int z0,
-                        int lane_u, int lane_h) {
-#pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    const int pc = wid * PER_WAVE + i;  // wave-uniform
-    const bool is_g = pc < PIECES / 2;
-    const int r = is_g ? pc : pc - PIECES / 2;
-    const int q = q0 + r;
-    const char* src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
-                           : reinterpret_cast<const char*>(p.eps16.data +
-                                                           (int64_t)min(q, rows - 1) * p.eps16.ld +
-                                                           2 * z0);
-    if (MPV_ABL & 128) continue;
-    lds_dma16(src, (uint32_t)(((lane_u ^ dr32_swz(r)) << 5) + lane_h), lds_addr(dst + pc * 1024));
-  }
-}
-
-template <int TM, int TN>
-struct Dr32Frag {
-  s16x8 ah[TM], al[TM], bh[TN], bl[TN];
-};
-
-// tile t = 32-column block index within the 256-column image
-template <int ROWB>
-MPV_DEV s16x8 dr32_frag(const char* img, int t, int plane, int lg, int tq, int tp) {
-  const int slice = 2 * t + (lg & 1);
-  const int U = (slice >> 1) * 4 + (slice & 1) + plane;
-  const int rA = 8 * (lg >> 1) + tq, rB = rA + 4;
-  return __builtin_shufflevector(tr_read(img, rA * ROWB + ((U ^ dr32_swz(rA)) << 5) + tp * 8),
-                                 tr_read(img, rB * ROWB + ((U ^ dr32_swz(rB)) << 5) + tp * 8), 0,
-                                 1, 2, 3, 4, 5, 6, 7);
-}
-
-template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(WM* WN * 64, 1) void dR32_kernel(Dr16Params p) {
-  constexpr int NW = WM * WN;
-  constexpr int BL = WM * TM * 32, BZ = WN * TN * 32;
-  static_assert(BL == 256 && BZ == 256, "256 x 256 tile");
-  constexpr int ROWB = BL * 4;
-  constexpr int IMG = kDr32KR * ROWB;   // 16 KB per operand
-  constexpr int STAGE = 2 * IMG;        // 32 KB
-  constexpr int PIECES = STAGE / 1024;  // 32 rows of 1 KB
-  static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
-  constexpr int PER_WAVE = PIECES / NW;
-  constexpr int P = kDr32NS - 1;        // stages in flight
-  __shared__ __attribute__((aligned(1024))) char smem[kDr32NS * STAGE];
-
-  int kc, tile;
-  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
-  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int tq = lr >> 2, tp = lr & 3;
-  const int rows = p.B * p.S;
-  const int q_begin = kc * p.rows_per_chunk;
-  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
-  const int lane_u = lane >> 1, lane_h = (lane & 1) * 16;
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[m][n][j] = 0.0f;
-
-  const int nst = (q_end - q_begin + kDr32KR - 1) / kDr32KR;
-  for (int j = 0; j < P && j < nst; ++j)
-    dr32_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDr32KR, rows, wid, l0, z0,
-                                 lane_u, lane_h);
-  for (int ci = 0; ci < nst; ++ci) {
-    wait_vmcnt_dyn(min(P - 1, nst - 1 - ci) * PER_WAVE);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();  // stage ci landed for every wave; all waves are done reading ci-1
-    if (ci + P < nst)
-      dr32_issue<PER_WAVE, PIECES>(p, smem + ((ci + P) % kDr32NS) * STAGE,
-                                   q_begin + (ci + P) * kDr32KR, rows, wid, l0, z0, lane_u,
-                                   lane_h);
-    const char* base = smem + (ci % kDr32NS) * STAGE;
-    Dr32Frag<TM, TN> f;
-#pragma unroll
-    for (int m = 0; m < TM; ++m) {
-      f.ah[m] = dr32_frag<ROWB>(base, wm * TM + m, 0, lg, tq, tp);
-      f.al[m] = dr32_frag<ROWB>(base, wm * TM + m, 2, lg, tq, tp);
-    }
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      f.bh[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 0, lg, tq, tp);
-      f.bl[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 2, lg, tq, tp);
-    }
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
-                                                           acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-      }
-  }
-  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
-  // D[i = l][j = z], 32x32 block: reg j -> row 8*(j/4) + 4*(lane/32) + j%4, col lane%32
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int l = l0 + (wm * TM + m) * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
-        const int zc = z0 + (wn * TN + n) * 32 + (lane & 31);
-        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][j] * inv;
-      }
-}
-
-// Staggered 32x32x16 dR: 16-row stages in a 4-deep ring, the two wave groups
-// (wm = 0, 1; paired on the SIMDs) one slot apart.  Group g does mem(j) in slot
-// 2j+g and mma(j) in slot 2j+g+1; each slot ends with one barrier.
-//   mem(j): LDS-DMA of this wave's share of stage j+3 into image (j+3)%4 (it held
-//           stage j-1, read in slots 2j-2 / 2j-1), fragment reads of stage j.
-//   mma(j): 24 MFMAs; then wait until this wave's pieces of stage j+2 landed,
-//           so stage j+2 is complete after the barrier that precedes its first
-//           read (slot 2j+4).
-// DMA is spread over every wave and every slot, with ~2 slot pairs of slack.
-template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(WM* WN * 64, 1) void dR32s_kernel(Dr16Params p) {
-  static_assert(WM == 2, "two wave groups");
-  constexpr int NW = WM * WN;
-  constexpr int BL = WM * TM * 32, BZ = WN * TN * 32;
-  static_assert(BL == 256 && BZ == 256, "256 x 256 tile");
-  constexpr int ROWB = BL * 4;
-  constexpr int IMG = kDr32KR * ROWB;   // 16 KB per operand
-  constexpr int STAGE = 2 * IMG;        // 32 KB
-  constexpr int PIECES = STAGE / 1024;  // 32 rows of 1 KB
-  static_assert(PIECES % NW == 0, "DMA pieces must split over waves");
-  constexpr int PER_WAVE = PIECES / NW;
-  __shared__ __attribute__((aligned(1024))) char smem[kDr32NS * STAGE];
-
-  int kc, tile;
-  decode_kc_tile(blockIdx.x, p.nKc, p.nLt * p.nZt, kc, tile);
-  const int l0 = (tile / p.nZt) * BL, z0 = (tile % p.nZt) * BZ;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int grp = wm;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int tq = lr >> 2, tp = lr & 3;
-  const int rows = p.B * p.S;
-  const int q_begin = kc * p.rows_per_chunk;
-  const int q_end = min(p.rows_pad, q_begin + p.rows_per_chunk);
-  const int lane_u = lane >> 1, lane_h = (lane & 1) * 16;
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc[m][n][j] = 0.0f;
-
-  const int nst = (q_end - q_begin + kDr32KR - 1) / kDr32KR;
-  for (int j = 0; j < 3 && j < nst; ++j)
-    dr32_issue<PER_WAVE, PIECES>(p, smem + j * STAGE, q_begin + j * kDr32KR, rows, wid, l0, z0,
-                                 lane_u, lane_h);
-  // stages 0 and 1 complete (own pieces; stage 2 may fly), then everyone: the
-  // loop's own waits start with stage 2 (end of mma(0))
-  wait_vmcnt_dyn(max(0, min(3, nst) - 2) * PER_WAVE);
-  barrier_raw();
-  if (grp == 1) barrier_raw();  // group 1 runs one slot behind
-  Dr32Frag<TM, TN> f;
-  for (int j = 0; j < nst; ++j) {
-    // ---- mem(j)
-    if (j + 3 < nst)
-      dr32_issue<PER_WAVE, PIECES>(p, smem + ((j + 3) & 3) * STAGE, q_begin + (j + 3) * kDr32KR,
-                                   rows, wid, l0, z0, lane_u, lane_h);
-    const char* base = smem + (j & 3) * STAGE;
-#pragma unroll
-    for (int m = 0; m < TM; ++m) {
-      f.ah[m] = dr32_frag<ROWB>(base, wm * TM + m, 0, lg, tq, tp);
-      f.al[m] = dr32_frag<ROWB>(base, wm * TM + m, 2, lg, tq, tp);
-    }
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      f.bh[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 0, lg, tq, tp);
-      f.bl[n] = dr32_frag<ROWB>(base + IMG, wn * TN + n, 2, lg, tq, tp);
-    }
-    lds_barrier();
-    // ---- mma(j)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.ah[m]), as_f16x8(f.bl[n]),
-                                                           acc[m][n], 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(f.al[m]), as_f16x8(f.bh[n]),
-                                                           acc[m][n], 0, 0, 0);
-      }
-    __builtin_amdgcn_s_setprio(0);
-    // own pieces of stage j+2 landed; stages j+3 (issued this round) may fly
-    if (j + 2 < nst) wait_vmcnt_dyn(min(1, nst - 1 - (j + 2)) * PER_WAVE);
-    barrier_raw();
-  }
-  if (grp == 0) barrier_raw();  // same barrier count for both groups
-  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int l = l0 + (wm * TM + m) * 32 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
-        const int zc = z0 + (wn * TN + n) * 32 + (lane & 31);
-        if (l < p.L && zc < p.z) p.slab[((int64_t)kc * p.L + l) * p.z + zc] = acc[m][n][j] * inv;
       }
 }
 
@@ -1231,16 +835,10 @@ constexpr int kDr16Tile = 256;  // 3xf16 dR tile: 256 x 256, 8 waves of 128 x 64
 // noise planes are padded to 128 columns instead of 256
 constexpr int kDr16TileSmall = 128;
 
-#ifndef MPV_DR_SMALL
-#define MPV_DR_SMALL 1  // 0: always the 256 tile (timing study)
-#endif
-#ifndef MPV_DR_SMALL_KC
-#define MPV_DR_SMALL_KC 2  // K chunks per CU for the 128 tile
-#endif
+constexpr int kDrSmallChunksPerCu = 2;  // K chunks per CU for the 128 tile
 
 static int dr16_tile(int64_t L, int64_t z) {
-  return (MPV_DR_SMALL && L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall
-                                                                       : kDr16Tile;
+  return (L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall : kDr16Tile;
 }
 
 static int num_cus() {
@@ -1268,8 +866,8 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.RPI = 256 / pl.TPR;
   // s-chunks: enough blocks for several rounds of resident blocks (short tail)
   int64_t want = cdiv(8192, B * pl.nLc);
-  if (MPV_ELEM_MINR > 0)  // but at least MPV_ELEM_MINR rows per thread (block setup amortised)
-    want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * MPV_ELEM_MINR));
+  // but at least kElemMinRows rows per thread (block setup amortised)
+  want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * kElemMinRows));
   if (want < 1) want = 1;
   const int64_t max_chunks = cdiv(S, pl.RPI);
   if (want > max_chunks) want = max_chunks;
@@ -1283,7 +881,7 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.rows_pad = (int)(cdiv(rows, kr) * kr);
   // split-K chunks: the 3xf16 kernel (1 workgroup per CU) gets one workgroup
   // per CU in a single wave of equal chunks; the fp32 kernel several per CU
-  int64_t kc = planes ? cdiv((dr_tile == kDr16Tile ? 1 : MPV_DR_SMALL_KC) * (int64_t)num_cus(), tiles)
+  int64_t kc = planes ? cdiv((dr_tile == kDr16Tile ? 1 : kDrSmallChunksPerCu) * (int64_t)num_cus(), tiles)
                       : cdiv(1536, tiles);
   const int64_t kc_max = cdiv(rows, 256);
   if (kc > kc_max) kc = kc_max;
@@ -1303,13 +901,6 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
 using namespace mpv;
 
 extern "C" {
-
-#if (MPV_ABL & 1024)
-int mpv_dbg_dr_stamps(void* host_out) {
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_dr_stamps), sizeof(g_dr_stamps)) == hipSuccess
-             ? 0 : 1;
-}
-#endif
 
 int64_t mpv_noise_plane_cols(const mpv_shape* shape) {
   if (check_shape(shape) != MPV_OK) return 0;
@@ -1397,17 +988,13 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.rows_per_chunk = pl.rows_per_chunk;
   ep.inv_S = 1.0f / (float)shape->S_total;
   const dim3 eg(B, pl.nSc, pl.nLc);
-  const bool vec = true;  // t_cols rows (the scalar instantiations stay for study)
-  if (want_planes) {
-    if (vec && pl.RPI == 1)
-      MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, true>), eg, dim3(256), 0, st, ep);
-    else if (vec)
-      MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, false>), eg, dim3(256), 0, st, ep);
-    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, true, false>), eg, dim3(256), 0, st, ep);
-  } else {
-    if (vec) MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false, false>), eg, dim3(256), 0, st, ep);
-    else MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<false, false, false>), eg, dim3(256), 0, st, ep);
-  }
+  // t_cols rows: 16-B aligned, whole float4 reads (VEC)
+  if (want_planes && pl.RPI == 1)
+    MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, true>), eg, dim3(256), 0, st, ep);
+  else if (want_planes)
+    MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, false>), eg, dim3(256), 0, st, ep);
+  else
+    MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false, false>), eg, dim3(256), 0, st, ep);
   if (int rc = check_launch("bwd_elem")) return rc;
   if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
     return rc;
@@ -1434,14 +1021,8 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       static_assert(kDr16Tile == 256 && kDr16TileSmall == 128, "launch configs below");
       if (pl.dr_tile == kDr16TileSmall)  // 128 x 128, 4 waves of 64 x 64, 2 x 32 KB stages
         MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 4, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
-      else if (MPV_DR_KIND == 3)
-        MPV_LAUNCH("dR_gemm", (dR32s_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
-      else if (MPV_DR_KIND == 2)
-        MPV_LAUNCH("dR_gemm", (dR32_kernel<2, 4, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
-      else if (MPV_DR_KIND == 1)
+      else  // 256 x 256, two wave groups one phase apart (dR16s)
         MPV_LAUNCH("dR_gemm", (dR16s_kernel<2, 4, 8, 4>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
-      else
-        MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 4, 8, 4, 2>), dim3((unsigned)blocks), dim3(512), 0, st, dp);
     } else {
       DrParams dp;
       dp.G = a->T;

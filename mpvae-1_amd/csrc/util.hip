@@ -304,22 +304,13 @@ __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int
 // the constant 2^12 (max |n| * s < 24200 < 65504).
 constexpr float kNoiseScale = 4096.0f;
 
-// A block makes MPV_NOISE_ROWS plane rows r = b*S + s; a thread makes 4
-// consecutive columns at a time (the 4 words of ONE Philox call when z % 4 ==
-// 0, else words of two calls).  Planes narrower than 4 x blockDim columns
-// give each row cols/4 threads and the block several rows at once.
-#ifndef MPV_NOISE_ROWS
-#define MPV_NOISE_ROWS 16  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
-#endif
-#ifndef MPV_NOISE_ABL
-#define MPV_NOISE_ABL 0  // timing study bits: 1 no Philox rounds, 2 no Box-Muller (wrong values)
-#endif
-#ifndef MPV_NOISE_CPT
-#define MPV_NOISE_CPT 8  // plane columns per thread: 8 (two 16-B stores; C4 1.78 -> 1.69 ms) or 4
-#endif
-#ifndef MPV_NOISE_NT
-#define MPV_NOISE_NT 0  // study: nontemporal stores of the noise planes (+38 %, off)
-#endif
+// A block makes kNoiseRows plane rows r = b*S + s; a thread makes 8
+// consecutive columns at a time (two groups of 4: the 4 words of ONE Philox
+// call when z % 4 == 0, else words of two calls), stored as two 16-B vectors.
+// Planes narrower than 8 x blockDim columns give each row cols/8 threads and
+// the block several rows at once.
+constexpr int kNoiseRows = 16;  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
+constexpr int kNoiseCols = 8;   // plane columns per thread (4: 1.78 ms, 8: 1.69 ms at C4)
 // Normals of columns c0 .. c0+3 (c0 % 4 == 0) of the plane row whose first
 // global element is e_row; zero past z.
 MPV_DEV void noise16_quad(int64_t e_row, int c0, int z, uint64_t offset, uint32_t k0, uint32_t k1,
@@ -332,17 +323,10 @@ MPV_DEV void noise16_quad(int64_t e_row, int c0, int z, uint64_t offset, uint32_
   if (c0 < z) {
     const int sh = (int)(e_row & 3);
     const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
-    const u32x4 w = (MPV_NOISE_ABL & 1)  // timing study: no Philox rounds
-                        ? u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32) ^ k0, k1, (uint32_t)ctr * 3u}
-                        : philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+    const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
     float a[8];
-    if (MPV_NOISE_ABL & 2) {  // timing study: no Box-Muller
-      a[0] = (float)(w.x & 0xffffu) * 1e-4f, a[1] = (float)(w.y & 0xffffu) * 1e-4f;
-      a[2] = (float)(w.z & 0xffffu) * 1e-4f, a[3] = (float)(w.w & 0xffffu) * 1e-4f;
-    } else {
-      box_muller(w.x, w.y, a[0], a[1]);
-      box_muller(w.z, w.w, a[2], a[3]);
-    }
+    box_muller(w.x, w.y, a[0], a[1]);
+    box_muller(w.z, w.w, a[2], a[3]);
     if (sh == 0) {
       v[0] = a[0], v[1] = a[1], v[2] = a[2], v[3] = a[3];
     } else {
@@ -360,8 +344,8 @@ MPV_DEV void noise16_quad(int64_t e_row, int c0, int z, uint64_t offset, uint32_
   }
 }
 
-// Columns c_first, c_first + c_step, ... (CPT each: 4, or 8 with 16-B stores)
-// of plane row r.
+// Columns c_first, c_first + c_step, ... (CPT each, two 16-B stores) of
+// plane row r.
 template <int CPT>
 MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_off, uint32_t k0,
                          uint32_t k1, uint64_t offset, int r, int c_first, int c_step) {
@@ -380,25 +364,14 @@ MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_
     uint16_t h[CPT], l[CPT];
 #pragma unroll
     for (int q = 0; q < CPT; ++q) split_f16(v[q], kNoiseScale, h[q], l[q]);
+    static_assert(CPT == 8, "two 16-B stores per thread");
     const int64_t o = chunked_index(r, out.ld, c0);
-    if constexpr (CPT == 8) {
-      const s16x8 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3],
-                     (short)h[4], (short)h[5], (short)h[6], (short)h[7]};
-      const s16x8 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3],
-                     (short)l[4], (short)l[5], (short)l[6], (short)l[7]};
-      *reinterpret_cast<s16x8*>(out.data + o) = hv;
-      *reinterpret_cast<s16x8*>(out.data + o + kLoOff) = lv;
-    } else {
-      const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-      const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
-      if (MPV_NOISE_NT) {
-        __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(out.data + o));
-        __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(out.data + o + kLoOff));
-      } else {
-        *reinterpret_cast<s16x4*>(out.data + o) = hv;
-        *reinterpret_cast<s16x4*>(out.data + o + kLoOff) = lv;
-      }
-    }
+    const s16x8 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3],
+                   (short)h[4], (short)h[5], (short)h[6], (short)h[7]};
+    const s16x8 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3],
+                   (short)l[4], (short)l[5], (short)l[6], (short)l[7]};
+    *reinterpret_cast<s16x8*>(out.data + o) = hv;
+    *reinterpret_cast<s16x8*>(out.data + o + kLoOff) = lv;
   }
 }
 
@@ -409,17 +382,17 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
                                                             const uint64_t* __restrict__ seed_dev) {
   philox_key(seed_dev, k0, k1);
   const int cols = (int)(out.ld >> 1);
-  const int r_end = min(rows, (int)(blockIdx.x + 1) * MPV_NOISE_ROWS);
-  constexpr int CPT = MPV_NOISE_CPT;
+  const int r_end = min(rows, (int)(blockIdx.x + 1) * kNoiseRows);
+  constexpr int CPT = kNoiseCols;
   const int tpr = min((int)blockDim.x, cols / CPT);  // threads per row
   if (tpr == (int)blockDim.x) {  // wide planes: the row (and its index math) is block-uniform
-    for (int r = blockIdx.x * MPV_NOISE_ROWS; r < r_end; ++r)
+    for (int r = blockIdx.x * kNoiseRows; r < r_end; ++r)
       noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, threadIdx.x * CPT,
                        blockDim.x * CPT);
   } else {  // narrow planes (C2, C3): several rows per pass of the block
     const int rpi = (int)blockDim.x / tpr;
     if ((int)threadIdx.x >= rpi * tpr) return;
-    for (int r = blockIdx.x * MPV_NOISE_ROWS + (int)threadIdx.x / tpr; r < r_end; r += rpi)
+    for (int r = blockIdx.x * kNoiseRows + (int)threadIdx.x / tpr; r < r_end; r += rpi)
       noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, ((int)threadIdx.x % tpr) * CPT,
                        tpr * CPT);
   }
@@ -554,9 +527,9 @@ static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
   MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
-  const int64_t tpr = out->ld / 2 / MPV_NOISE_CPT;  // threads per plane row
+  const int64_t tpr = out->ld / 2 / kNoiseCols;  // threads per plane row
   const unsigned threads = tpr >= 256 ? 256 : (unsigned)(cdiv(tpr, 64) * 64);
-  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(rows, MPV_NOISE_ROWS)),
+  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(rows, kNoiseRows)),
              dim3(threads), 0, s, *out, (int)shape->S_local, (int)shape->B, (int)shape->z,
              shape->s_offset, (uint32_t)seed, (uint32_t)(seed >> 32), offset, (int)rows, seed_dev);
   return check_launch("noise_philox_f16");

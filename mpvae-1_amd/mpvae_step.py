@@ -78,6 +78,7 @@ class TrainStep:
         dev = self.params[0].device
         self.updates = torch.zeros((), dtype=torch.int64, device=dev)
         self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.graph = None
         self.label = self.feat = self.out = None
 
@@ -91,16 +92,22 @@ class TrainStep:
         res = mpvae.compute_loss(label, *out, self.model.r_sqrt_sigma, self.args)
         res[0].backward()
         torch.nn.utils.clip_grad_norm_(self.params, self.max_grad_norm, foreach=True)
-        grads = [p.grad for p in self.params if p.grad is not None]
-        peaks = torch._foreach_norm(grads, float("inf"))  # NaN-propagating max |g|
-        bad = torch.stack([~torch.isfinite(pk) for pk in peaks]).any()
-        self.found_inf.copy_(bad.to(torch.float32))
+        # finite gate: the AMP multi-tensor check (one launch per dtype) sets
+        # found_inf if any gradient holds a NaN / inf; its unscale by 1.0
+        # leaves every value as it is
+        self.found_inf.zero_()
+        by_dtype = {}
+        for p in self.params:
+            if p.grad is not None:
+                by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
+        for grads in by_dtype.values():
+            torch._amp_foreach_non_finite_check_and_unscale_(grads, self.found_inf, self._one)
         self.opt.found_inf = self.found_inf
         try:
             self.opt.step()
         finally:
             del self.opt.found_inf
-        self.updates.add_(1 - bad.to(torch.int64))
+        self.updates.add_(1 - self.found_inf.to(torch.int64))
         return res
 
     def __call__(self, label, feat):
