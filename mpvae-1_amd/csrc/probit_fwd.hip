@@ -963,10 +963,9 @@ MPV_DEV bool fwd_tile_soft(const FwdParams& p, int b, int n0, int nthreads) {
   return __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
 }
 
-// The 128 x 128 transposed tile (48 < L <= 128 on the 3xf16 path): 4 waves of
-// 64 labels x 64 samples, 2-stage ring, two workgroups per CU.  The waves of
-// the second half issue the stage DMA at static priority 1 (the other half
-// starts its MFMAs at the barrier).
+// The transposed tile for 48 < L <= 128 on the 3xf16 path (launch_fwd: 128 x
+// 128, 8 waves), 2-stage ring.  The waves of the second half issue the stage
+// DMA at static priority 1 (the other half starts its MFMAs at the barrier).
 template <int WL, int WS, int TL, int TS, int NSTAGE>
 __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
   constexpr int NW = WL * WS;
@@ -1307,8 +1306,15 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
         MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3>), grid, dim3(512), 0, st, p);
         break;
-      default:  // 128 x 128 tile: transposed accumulators (cheap epilogue)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 2, 4, 4, 2>), grid, dim3(256), 0, st, p);
+      default:
+        // 128 x 128 tile, transposed accumulators (cheap epilogue): 8 waves of
+        // 32 labels x 64 samples, one workgroup per CU.  The 4-wave version
+        // (64 x 64 per wave, two workgroups per CU) ran 0.031 ms faster at C3
+        // but was not repeatable: 10-13 % of its launches at C3 differed in
+        // one label-branch row statistic of a 16-sample block (never with one
+        // workgroup per CU, the same code padded to 81 KB of LDS; DESIGN.md
+        // section 4, tools/repeat_probe.py)
+        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<4, 2, 2, 4, 2>), grid, dim3(512), 0, st, p);
         break;
     }
   }

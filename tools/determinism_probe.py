@@ -69,13 +69,15 @@ neg = (y == 0).double()[:, None, :]
 pos = (y == 1).double()[:, None, :]
 Nref = (torch.exp(5 * E) * neg).sum(-1)                           # (B, S)
 Pref = (torch.exp(-5 * E) * pos).sum(-1)
-for k, b, s in idx[:40].tolist():
-    ref = {2: Pref, 3: Nref}.get(k)
+LPref = (torch.log(E) * pos + torch.log(1 - E) * neg).sum(-1)
+for k, b, s in idx[:60].tolist():
+    ref = {0: LPref, 2: Pref, 3: Nref}.get(k)
     print(f"  k={k} b={b} s={s}: runs {[round(float(r[k, b, s]), 4) for r in rs]}"
           + (f" ref {float(ref[b, s]):.4f}" if ref is not None else ""))
 # which lanes / rows: s mod 128 (position in the tile) histogram
 if idx.shape[0]:
     pos_in_tile = (idx[:, 2] % 128).tolist()
+    print("sample rows (s):", sorted(set(idx[:, 2].tolist()))[:80])
     print("positions in 128-tile:", sorted(set(pos_in_tile))[:64])
     print("batch rows:", sorted(set(idx[:, 1].tolist()))[:64])
     print("stats k:", sorted(set(idx[:, 0].tolist())))
