@@ -836,6 +836,7 @@ constexpr int kDr16Tile = 256;  // 3xf16 dR tile: 256 x 256, 8 waves of 128 x 64
 constexpr int kDr16TileSmall = 128;
 
 constexpr int kDrSmallChunksPerCu = 2;  // K chunks per CU for the 128 tile
+constexpr int64_t kDrMaxChunkRows = 131072;  // longest split-K chunk (sample rows)
 
 static int dr16_tile(int64_t L, int64_t z) {
   return (L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall : kDr16Tile;
@@ -883,6 +884,11 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   // per CU in a single wave of equal chunks; the fp32 kernel several per CU
   int64_t kc = planes ? cdiv((dr_tile == kDr16Tile ? 1 : kDrSmallChunksPerCu) * (int64_t)num_cus(), tiles)
                       : cdiv(1536, tiles);
+  // but no K chunk longer than kDrMaxChunkRows: one fp32 accumulator per output
+  // over 4.2 M rows (C5 on one GPU: 256 tiles, so one chunk each) drifted 1e-4
+  // (normwise) between two shardings of the same sum; chunks of <= 128 K rows
+  // keep it at the C4 level (< 1e-5), the chunks summed in a fixed order
+  kc = std::max<int64_t>(kc, cdiv(rows, kDrMaxChunkRows));
   const int64_t kc_max = cdiv(rows, 256);
   if (kc > kc_max) kc = kc_max;
   if (kc < 1) kc = 1;
