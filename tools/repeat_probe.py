@@ -22,15 +22,31 @@ be = HipShardBackend()
 shape = be.shape(S, S, 0, B, L, z)
 Rop = be.prepare_R(R)
 eps = be.make_noise(shape, DEV, 42, 0)
-first = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep_T)["rowstat"].clone()
-bad_runs, bad_k = 0, set()
+gscal = torch.tensor([1.0, 0.0, 0.0, 0.0, 0.0, 0.0], device=DEV)
+bwd = os.environ.get("PROBE_BWD") == "1"
+
+
+def one(keep):
+    loc = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep or bwd)
+    if not bwd:
+        return loc["rowstat"].clone(), None
+    saved = dict(y=y, fe_out=fe, fx_out=fx, eps=eps, T=loc["T"], rowstat=loc["rowstat"],
+                 bstat=loc["bstat"])
+    flat, _, _ = be.backward_local(shape, saved, gscal, 0b000001, None, None, 0.1, 200.0, True)
+    return loc["rowstat"].clone(), flat.clone()
+
+
+first, gfirst = one(True)
+bad_runs, bad_k, bad_g = 0, set(), 0
 for _ in range(runs):
-    rs = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep_T)["rowstat"]
+    rs, gr = one(keep_T)
     d = rs != first
     if d.any():
         bad_runs += 1
         bad_k |= set(torch.nonzero(d)[:, 0].tolist())
+    if bwd and not torch.equal(gr, gfirst):
+        bad_g += 1
 torch.cuda.synchronize()
-print(f"{os.environ.get('MPVAE_HIP_LIB', 'default').split('/')[-2]} B={B} S={S} L={L}: "
+print(f"{os.environ.get('MPVAE_HIP_LIB', 'x/default/x').split('/')[-2]} B={B} S={S} L={L}: "
       f"keep_T={keep_T} {bad_runs}/{runs} runs differ, stats {sorted(bad_k)}"
       + (f"; backward: {bad_g}/{runs} differ" if bwd else ""), flush=True)
