@@ -480,9 +480,13 @@ def test_gemm_modes_agree_at_c4_dims():
         res[gemm] = [_np(o) for o in out] + [_np(x.grad) for x in leaves]
     names = OUTS + ["d" + k for k in ["fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu",
                                        "fx_logvar", "r_sqrt_sigma"]]
-    for k, a, b in zip(names, res["f16x3"], res["f32"]):
-        tol = FWD_RTOL if not k.startswith("d") else 2e-4
-        assert rel_err(a, b) <= tol, (k, rel_err(a, b))
+    errs = {k: rel_err(a, b) for k, a, b in zip(names, res["f16x3"], res["f32"])}
+    record("gemm_modes_c4_dims", errs)
+    for k, e in errs.items():
+        # gradients: the two modes' t differ by fp32 rounding, which the
+        # headline coefficients condition at ~1e-4 (HEADLINE_GRAD_RTOL)
+        tol = FWD_RTOL if not k.startswith("d") else HEADLINE_GRAD_RTOL
+        assert e <= tol, (k, e)
 
 
 def test_test_mode_forward_only_large_s():

@@ -15,14 +15,17 @@ scipy's erf disagree there by up to 1.3e-2 in the gradient.  That fixture is
 checked at the looser level.
 """
 
-FWD_RTOL = 2e-5
-GRAD_RTOL = 5e-5
+# Each tolerance sits at 1-5x the largest error measured on the MI355X for the
+# cases it covers (profiles/r03_parity_errors.json, recorded by these tests
+# with MPVAE_RECORD_ERRS set); the comment gives that measurement.
+FWD_RTOL = 2e-6    # measured <= 4.8e-7 (golden, random, C2/C3 full size, eval 10000)
+GRAD_RTOL = 5e-5   # measured <= 4.1e-5 (random cases with K ~ 1000 noise dims; golden <= 6.3e-6)
 # Long noise GEMMs (z = 4096): the gradient w.r.t. fe_out / fx_out / R is
 # conditioned at the 1e-4 level by the fp32 rounding of t = eps . R^T alone:
 # the oracle with t from an fp32 sgemm (as the reference's own fp32
 # tensordot) instead of fp64 accumulation moves d fx_out by 1.05e-4 and dR by
 # 6.1e-5 on the test_random_against_oracle case (4096, 4096, 1, 40) --
-# measured, DESIGN.md section 4.  Allowed: 5x that spread.
+# measured, DESIGN.md section 4.  Measured here: 1.7e-4 (f16x3), 6.8e-5 (f32).
 LONG_K_GRAD_RTOL = 5e-4
 # The headline coefficients (nll_coeff 0.1, c_coeff 200, L = z = 1024) with
 # total_loss as the objective: the fp32 rounding of t = eps . R^T alone moves
@@ -31,12 +34,14 @@ LONG_K_GRAD_RTOL = 5e-4
 # d fe_out 1.6e-4 on bench.py's B = 512, S = 2 slice; 8e-6 at B = 64, S = 16),
 # and the reference restated in torch-CPU sits 1.9e-3 (d fe_out) / 3.9e-4 (dR)
 # from the oracle (tests/test_oracle_golden.py pins it: its fp32 1 - E near
-# E -> 1).  Stated: 1e-3, i.e. at least as close to the oracle as the reference
-# itself.  Measured on the GPU: <= 1.4e-4 (f16x3; reproduced to 3 digits by a
-# numpy emulation of its arithmetic: 3xf16 products added to the fp32
+# E -> 1).  Measured on the GPU: <= 1.4e-4 (f16x3; reproduced to 3 digits by
+# a numpy emulation of its arithmetic: 3xf16 products added to the fp32
 # accumulator term by term), <= 3e-5 (exact-fp32 MFMA mode).
-HEADLINE_GRAD_RTOL = 1e-3
-EXTREME_FWD_RTOL = 1e-3
+HEADLINE_GRAD_RTOL = 5e-4
+# The extreme-logit fixture (|u| up to ~20): E near the 0.5e-6 floor, where
+# torch-CPU's and scipy's erf disagree by up to 1.3e-2 in the gradient
+# (module docstring).  Measured: forward 3.6e-5, gradients 1.3e-2.
+EXTREME_FWD_RTOL = 1.5e-4
 EXTREME_GRAD_RTOL = 5e-2
 
 
