@@ -21,9 +21,6 @@
 // b), so fe/fx/y of the epilogue are per-lane constants and the column sums
 // over s stay in registers until the workgroup ends.  Workgroups sharing eps
 // rows (same b and s-chunk, other label tiles) get ids equal mod 8: one XCD.
-#include <cstdlib>
-#include <cstring>
-
 #include "abi_util.h"
 #include "mpv_common.h"
 
@@ -56,9 +53,6 @@ struct FwdParams {
 constexpr int kCombineThreads = 1024;  // fwd_combine: one block per batch row
 constexpr int kFwdWant = 2048;         // target workgroup count of the forward grid (s-chunking)
 constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
-#ifndef FWDW_FILL
-#define FWDW_FILL 2  // probit_fwd16w: VALU instructions scheduled after each MFMA
-#endif
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
@@ -1158,302 +1152,6 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
 }
 
-// ------------- 3xf16, epilogue overlapped with the next tile (probit_fwd16w)
-// The 256-label x 128-sample tile of probit_fwd16a on ONE wave per SIMD (4
-// waves, up to 512 registers each): wave w owns labels [64w, 64w+64) and all
-// 128 samples.  Two accumulator sets: the K loop of tile i accumulates into
-// `acc` while the epilogue of tile i-1 runs from `pacc`, one unit per K stage
-// (label group mg x sample block n: 4 labels x 1 sample per lane, both
-// branches), its VALU interleaved with the stage's 96 MFMAs.  In probit_fwd16a
-// every wave reaches the epilogue together and the matrix pipe idles for a
-// third of each tile.  Row statistics leave per wave (rowpart holds 4
-// partials per label tile, summed by fwd_combine), so the epilogue has no
-// cross-wave step and no barrier of its own.  32 units per tile: needs
-// nK >= 32 (z > 992); the last tile's epilogue runs after the loop.
-namespace fwdw {
-constexpr int NW = 4, TL = 4, TS = 8, BM = 128, BN = 256, NSTAGE = 3, UNITS = TL * TS;
-constexpr int STAGE = (BM + BN) * kRowB;  // 48 KB
-constexpr int CACC = BN * 2;             // floats: column sums (label, feature)
-}  // namespace fwdw
-
-// Per-label constants of label group mg for this lane (4 labels lb .. lb+3).
-struct FwdwCols {
-  f32x2 fex[4];                   // (fe, fx) x kZq
-  f32x2 qa2[2], qb2[2], sga2[2], sgb2[2], wpos2[2], wneg2[2];
-  f32x4 y4;
-};
-
-MPV_DEV void fwdw_cols(FwdwCols& c, const float* cols, int lb) {
-  using namespace fwdw;
-  const f32x4 pa = *reinterpret_cast<const f32x4*>(cols + 2 * lb);
-  const f32x4 pb = *reinterpret_cast<const f32x4*>(cols + 2 * lb + 4);
-  c.fex[0] = f32x2{pa[0], pa[1]};
-  c.fex[1] = f32x2{pa[2], pa[3]};
-  c.fex[2] = f32x2{pb[0], pb[1]};
-  c.fex[3] = f32x2{pb[2], pb[3]};
-  c.y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
-  const f32x4 qa = *reinterpret_cast<const f32x4*>(cols + kCqa * BN + lb);
-  const f32x4 qb = *reinterpret_cast<const f32x4*>(cols + kCqb * BN + lb);
-  const f32x4 sga = *reinterpret_cast<const f32x4*>(cols + kCsga * BN + lb);
-  const f32x4 sgb = *reinterpret_cast<const f32x4*>(cols + kCsgb * BN + lb);
-  const f32x4 wpos = *reinterpret_cast<const f32x4*>(cols + kCwpos * BN + lb);
-  const f32x4 wneg = *reinterpret_cast<const f32x4*>(cols + kCwneg * BN + lb);
-  c.qa2[0] = f32x2{qa[0], qa[1]}, c.qa2[1] = f32x2{qa[2], qa[3]};
-  c.qb2[0] = f32x2{qb[0], qb[1]}, c.qb2[1] = f32x2{qb[2], qb[3]};
-  c.sga2[0] = f32x2{sga[0], sga[1]}, c.sga2[1] = f32x2{sga[2], sga[3]};
-  c.sgb2[0] = f32x2{sgb[0], sgb[1]}, c.sgb2[1] = f32x2{sgb[2], sgb[3]};
-  c.wpos2[0] = f32x2{wpos[0], wpos[1]}, c.wpos2[1] = f32x2{wpos[2], wpos[3]};
-  c.wneg2[0] = f32x2{wneg[0], wneg[1]}, c.wneg2[1] = f32x2{wneg[2], wneg[3]};
-}
-
-// One epilogue unit: t of 4 labels (lb .. lb+3) x this lane's sample s, both
-// branches.  The same arithmetic as fwd_tile_epilogue_t's inner loop.
-template <bool SOFT>
-MPV_DEV void fwdw_unit(const FwdParams& p, f32x4 t4, const FwdwCols& c, int b, int s, bool own,
-                       int n0, int lb, f32x2& sl, f32x2& sp, f32x2& sn, f32x2 (&ce)[4]) {
-  const int S = p.S, L = p.L;
-  if (!(MPV_ABL & 2) && p.T != nullptr && own) {
-    float* row = p.T + ((int64_t)b * S + s) * p.ldT + n0;
-    if (n0 + lb < L) {  // t_cols rows: the pad labels' t (0) may be written
-      *reinterpret_cast<f32x4*>(row + lb) = t4;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (n0 + lb + i < L) row[lb + i] = t4[i];
-    }
-  }
-  const float wr = own ? 1.0f : 0.0f;
-  f32x2 zq[4], w4[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) zq[i] = pk_fma(splat2(t4[i]), splat2(kZq), c.fex[i]);
-  probit_w2xN_zq<4>(zq, w4);
-  f32x2 q[4], r[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    q[i] = (i & 1) ? pk_fma_bc<1>(w4[i], c.qa2[i >> 1], c.qb2[i >> 1])
-                   : pk_fma_bc<0>(w4[i], c.qa2[i >> 1], c.qb2[i >> 1]);
-    const f32x2 a = (i & 1) ? pk_fma_bc<1>(w4[i], c.sga2[i >> 1], c.sgb2[i >> 1])
-                            : pk_fma_bc<0>(w4[i], c.sga2[i >> 1], c.sgb2[i >> 1]);
-    r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-  }
-  const f32x2 q4 = (q[0] * q[1]) * (q[2] * q[3]);
-  f32x2 lp = f32x2{__builtin_amdgcn_logf(q4.x), __builtin_amdgcn_logf(q4.y)};
-  if (SOFT) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float y = c.y4[i];
-      if (n0 + lb + i < L && !(y == 0.0f || y == 1.0f)) {
-        const f32x2 E = pk_fma(w4[i], splat2(kEh), splat2(kC0));
-        lp.x += y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
-        lp.y += y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
-      }
-    }
-  }
-  sl = sl + lp;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i & 1)
-      pk_fma2_acc_bc<1>(c.wpos2[i >> 1], c.wneg2[i >> 1], r[i], sp, sn);
-    else
-      pk_fma2_acc_bc<0>(c.wpos2[i >> 1], c.wneg2[i >> 1], r[i], sp, sn);
-    ce[i] = pk_fma(splat2(wr), w4[i], ce[i]);
-  }
-}
-
-// One K stage of a wave's 64 x 128 block: the R fragments of its 4 label
-// blocks, then per sample block its eps fragments and 3 MFMAs per label block
-// (fragments just in time: 48 VGPRs instead of 96).
-MPV_DEV void fwdw_stage_mma(f32x4 (&acc)[fwdw::TL][fwdw::TS], const char* base, int wl, int lr,
-                            int coh, int col) {
-  using namespace fwdw;
-  s16x8 rh[TL], rl[TL];
-#pragma unroll
-  for (int m = 0; m < TL; ++m) {
-    const int off = (BM + (wl * TL + m) * 16 + lr) * kRowB;
-    rh[m] = *reinterpret_cast<const s16x8*>(base + off + coh);
-    rl[m] = *reinterpret_cast<const s16x8*>(base + off + col);
-  }
-#pragma unroll
-  for (int n = 0; n < TS; ++n) {
-    const int off = (n * 16 + lr) * kRowB;
-    const s16x8 eh = *reinterpret_cast<const s16x8*>(base + off + coh);
-    const s16x8 el = *reinterpret_cast<const s16x8*>(base + off + col);
-#pragma unroll
-    for (int m = 0; m < TL; ++m) {
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rh[m]), as_f16x8(eh), acc[m][n],
-                                                         0, 0, 0);
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rh[m]), as_f16x8(el), acc[m][n],
-                                                         0, 0, 0);
-      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rl[m]), as_f16x8(eh), acc[m][n],
-                                                         0, 0, 0);
-    }
-  }
-}
-
-template <bool SOFT>
-MPV_DEV void fwdw_main(const FwdParams& p, char* smem, float* cacc, const float* cols, int b,
-                       int nt, int sc) {
-  using namespace fwdw;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wl = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane & 15, lg = lane >> 4;
-  const int S = p.S, n0 = nt * BN;
-  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
-  const int nK = (p.z + kKC - 1) / kKC;  // >= 32 (host check)
-  const int sw = (lr >> 1) & 7;
-  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
-  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
-  const int nPart = p.nNt * NW, part = nt * NW + wl;  // rowpart partials: one per wave
-  Fwd16Dma<BM, BN, NW> dma;
-  dma.init(p, t_begin, b, n0, wl, lane);
-#pragma unroll
-  for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
-  const int pieces = dma.per_wave();
-
-  f32x4 acc[TL][TS], pacc[TL][TS];
-  f32x2 sl[TS], sp[TS], sn[TS], ce[4];
-#pragma unroll
-  for (int n = 0; n < TS; ++n) sl[n] = sp[n] = sn[n] = splat2(0.0f);
-  int gs = 0;
-  int prev_s0 = 0, prev_own = 0;
-  float ecount = 0.0f;  // C0 x the previous tile's own rows (column sums' constant part)
-
-  // one K stage: its DMA landed, one barrier, the next stage streams
-  auto stage_head = [&]() {
-    wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * pieces);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-    dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
-              t_end, nK, b);
-  };
-  auto stage_mma = [&]() { fwdw_stage_mma(acc, smem + (gs % NSTAGE) * STAGE, wl, lr, coh, col); };
-  // row statistics of sample block n (all label groups done): sum over the
-  // lane rows, this wave's partial out
-  auto publish = [&](int n) {
-    float v[6] = {sl[n].x * 0.6931471805599453f, sl[n].y * 0.6931471805599453f, sp[n].x,
-                  sn[n].x, sp[n].y, sn[n].y};
-    sum_lanegroups_n<6>(v);
-    const int s = prev_s0 + n * 16 + lr;
-    if (lg == 0 && s >= prev_own && s < S) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k)
-        p.rowpart[(((int64_t)k * nPart + part) * p.B + b) * S + s] = v[k];
-    }
-    sl[n] = sp[n] = sn[n] = splat2(0.0f);
-  };
-  // after the 8 units of label group mg: its column sums into cacc (this
-  // wave's own labels), the remaining groups rotate down
-  auto group_tail = [&](int mg) {
-    const int lb = (wl * TL + mg) * 16 + lg * 4;
-    float cs[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      cs[2 * i] = ce[i].x;
-      cs[2 * i + 1] = ce[i].y;
-      ce[i] = splat2(0.0f);
-    }
-    row16_sum_to_lane15_n<8>(cs);
-    if (lr == 15) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float* c = cacc + (lb + i) * 2;
-        c[0] += fmaf(kEh, cs[2 * i], ecount);
-        c[1] += fmaf(kEh, cs[2 * i + 1], ecount);
-      }
-    }
-#pragma unroll
-    for (int mm = 0; mm + 1 < TL; ++mm)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) pacc[mm][n] = pacc[mm + 1][n];
-  };
-
-  bool have_prev = false;
-  for (int st = t_begin; st <= t_end; ++st) {
-    const bool mf = st < t_end;  // uniform: a K loop to run (else: drain the last epilogue)
-    const int s0 = mf ? fwd_tile_s0<BM>(st, S) : 0;
-#pragma unroll
-    for (int m = 0; m < TL; ++m)
-#pragma unroll
-      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (have_prev) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ce[i] = splat2(0.0f);
-#pragma unroll 1
-      for (int mg = 0; mg < TL; ++mg) {
-        const int lb = (wl * TL + mg) * 16 + lg * 4;
-        // the label group's constants are re-read from LDS per unit: held
-        // across the 8 units they cost 32 VGPRs
-#define FWDW_STEP(N)                                                                           \
-  do {                                                                                         \
-    const int s_ = prev_s0 + (N) * 16 + lr;                                                    \
-    const bool own_ = s_ >= prev_own && s_ < S;                                                \
-    FwdwCols cc;                                                                               \
-    fwdw_cols(cc, cols, lb);                                                                   \
-    if (mf) {                                                                                  \
-      stage_head();                                                                            \
-      if (!(MPV_ABL & 64))                                                                     \
-        fwdw_unit<SOFT>(p, pacc[0][N] * scale, cc, b, s_, own_, n0, lb, sl[N], sp[N], sn[N], ce); \
-      fwdw_stage_mma(acc, smem + (gs % NSTAGE) * STAGE, wl, lr, coh, col);                     \
-      if (FWDW_FILL > 0) {                                                                     \
-        _Pragma("unroll") for (int i = 0; i < 96; ++i) {                                       \
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                   \
-          __builtin_amdgcn_sched_group_barrier(0x002, FWDW_FILL > 0 ? FWDW_FILL : 1, 0);       \
-        }                                                                                      \
-      }                                                                                        \
-      ++gs;                                                                                    \
-    } else {                                                                                   \
-      fwdw_unit<SOFT>(p, pacc[0][N] * scale, cc, b, s_, own_, n0, lb, sl[N], sp[N], sn[N], ce); \
-    }                                                                                          \
-    if (mg == TL - 1) publish(N);                                                              \
-  } while (0)
-        FWDW_STEP(0); FWDW_STEP(1); FWDW_STEP(2); FWDW_STEP(3);
-        FWDW_STEP(4); FWDW_STEP(5); FWDW_STEP(6); FWDW_STEP(7);
-#undef FWDW_STEP
-        group_tail(mg);
-      }
-      if (mf)
-        for (int kc = UNITS; kc < nK; ++kc, ++gs) {
-          stage_head();
-          stage_mma();
-        }
-    } else if (mf) {  // first tile: nothing to overlap
-      for (int kc = 0; kc < nK; ++kc, ++gs) {
-        stage_head();
-        stage_mma();
-      }
-    }
-    if (mf) {
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TS; ++n) pacc[m][n] = acc[m][n];
-      prev_s0 = s0;
-      prev_own = st * BM;
-      ecount = kC0 * (float)max(0, min(S, s0 + BM) - max(prev_own, s0));
-    }
-    have_prev = mf;
-  }
-}
-
-__global__ __launch_bounds__(256, 1) void probit_fwd16w_kernel(FwdParams p) {
-  using namespace fwdw;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (CACC + kColsT * BN) * 4];
-  float* cacc = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  float* cols = cacc + CACC;
-  int g, nt;
-  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
-  const int b = g / p.nSc, sc = g % p.nSc;
-  const int n0 = nt * BN;
-  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
-  for (int i = threadIdx.x; i < CACC; i += NW * 64) cacc[i] = 0.0f;
-  // readfirstlane: the branch around the whole main loop must be uniform
-  if (fwd_tile_soft<BN>(p, b, n0, NW * 64))  // (its __syncthreads_or publishes cols / cacc)
-    fwdw_main<true>(p, smem, cacc, cols, b, nt, sc);
-  else
-    fwdw_main<false>(p, smem, cacc, cols, b, nt, sc);
-  fwd16t_colpart<1, BN>(p, cacc, b, sc, n0, NW * 64);
-}
-
 // One block per batch row b.  rowpart -> rowstat, bstat.
 __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restrict__ y,
                                                          const float* __restrict__ rowpart,
@@ -1560,20 +1258,8 @@ __global__ __launch_bounds__(1024) void finalize_kernel(mpv_final_args a, int B,
 struct FwdPlan {
   int cfg;  // tile configuration, see launch_fwd
   int BM, BN, nNt, nSt, nSc, tps;
-  bool overlap;  // cfg 3 on probit_fwd16w (epilogue overlapped with the next tile)
-  int parts;     // rowpart partials per label tile (one per probit_fwd16w wave)
   size_t rowpart_bytes, colpart_bytes;
 };
-
-// probit_fwd16w (study, off): MPVAE_FWD_KERNEL=16w selects it for the
-// 256-label tile when z gives it >= 32 K stages.  C4 forward 16.9 vs 13.2 ms
-// (probit_fwd16a): its one-wave-per-SIMD K loop alone runs 13.1 ms
-// (probit_fwd16a's two-wave K loop: 9.6), MFMA + fragment reads without the
-// DMA 10.2 ms (7.4) -- DESIGN.md section 3, round 3.
-static bool fwd_overlap_enabled() {
-  const char* e = getenv("MPVAE_FWD_KERNEL");
-  return e && strcmp(e, "16w") == 0;
-}
 
 static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
@@ -1594,10 +1280,7 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   if (want > pl.nSt) want = pl.nSt;
   pl.tps = (int)cdiv(pl.nSt, want);
   pl.nSc = (int)cdiv(pl.nSt, pl.tps);
-  pl.overlap = f16 && pl.cfg == 3 && cdiv(s->z, kKC) >= fwdw::UNITS && fwd_overlap_enabled();
-  pl.parts = pl.overlap ? fwdw::NW : 1;
-  pl.rowpart_bytes =
-      align_up(sizeof(float) * 6 * (size_t)pl.nNt * pl.parts * s->B * s->S_local, 256);
+  pl.rowpart_bytes = align_up(sizeof(float) * 6 * (size_t)pl.nNt * s->B * s->S_local, 256);
   pl.colpart_bytes = pl.nSc > 1 ? align_up(sizeof(float) * (size_t)pl.nSc * 2 * s->B * s->L, 256) : 0;
   return pl;
 }
@@ -1620,11 +1303,8 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 0:  // BN 48, 4 waves, 3-stage ring (66 KB LDS: 2 workgroups per CU)
         MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 3>), grid, dim3(256), 0, st, p);
         break;
-      case 3:
-        if (pl.overlap)  // 256 labels x 128 samples, 4 waves, epilogue under the next tile's MFMAs
-          MPV_LAUNCH("probit_fwd", probit_fwd16w_kernel, grid, dim3(256), 0, st, p);
-        else  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
-          MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3>), grid, dim3(512), 0, st, p);
+      case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
+        MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3>), grid, dim3(512), 0, st, p);
         break;
       default:
         // 128 x 128 tile, transposed accumulators (cheap epilogue): 8 waves of
@@ -1717,7 +1397,7 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
   MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(kCombineThreads), 0, st, a->y,
-             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt * pl.parts);
+             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
   if (int rc = check_launch("fwd_combine")) return rc;
   if (pl.nSc > 1) {
     if (int rc = launch_sum_slabs(p.colpart, pl.nSc, 2 * shape->B * shape->L, a->colsum, MPV_F32, st))
