@@ -87,8 +87,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--steps", type=int, default=50)
+    # torch's BLAS backend for the nn.Linear GEMMs: hipBLASLt (torch's default on
+    # MI355X) or rocBLAS ("cublas" in torch's naming)
+    ap.add_argument("--blas", default=None, choices=["cublaslt", "cublas"])
     cli = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if cli.blas:
+        torch.backends.cuda.preferred_blas_library(cli.blas)
 
     args, model, opt, label, feat = build(cli.config, dev, fused=False)
     for _ in range(3):
@@ -134,7 +139,8 @@ def main():
         kernels = {"error": repr(e)[:300]}
 
     F_, L, z, d, B, S, nllc, cc, lr = CONFIGS[cli.config]
-    print(json.dumps({"config": {"name": cli.config, "feature_dim": F_, "label_dim": L, "z_dim": z,
+    print(json.dumps({"blas": str(torch.backends.cuda.preferred_blas_library()),
+                      "config": {"name": cli.config, "feature_dim": F_, "label_dim": L, "z_dim": z,
                                  "latent_dim": d, "batch": B, "n_train_sample": S,
                                  "nll_coeff": nllc, "c_coeff": cc, "lr": lr},
                       "steps": cli.steps, "eager_ms": round(eager_ms, 4),
