@@ -1,0 +1,51 @@
+#!/bin/bash
+# Round-3 evidence on one GPU box, in two calls (each fits gpurun's limit):
+#   PART=tests tools/r03_final.sh   GPU suite (measured errors recorded), smoke,
+#                                   repeatability probes of the dispatched tiles
+#   PART=bench tools/r03_final.sh   bench lines, train-step profiles, rocprof
+# Stops at the first step that fails, times out or crashes.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+O="$R/gpurun_out/${OUT:-r3final}"
+mkdir -p "$O"
+cd "$R"
+step() {  # name, timeout, command...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$O/$n.out" 2> "$O/$n.err"
+  local rc=$?
+  echo "[$n] rc=$rc"
+  [ $rc -eq 0 ] || { tail -30 "$O/$n.out"; tail -10 "$O/$n.err"; exit $rc; }
+}
+b() {  # name, bench args...
+  local n=$1; shift
+  step "$n" 400 python bench.py "$@"
+  python -c "import json;d=json.load(open('$O/$n.out'));print('$n',round(d['ms_per_step'],4),'%.4g'%d['value'],d['roofline'].get('frac'))"
+}
+if [ "$PART" = tests ]; then
+  MPVAE_RECORD_ERRS="$O/parity_errs.jsonl" step tests 1000 python -u -m pytest tests -m gpu -q \
+    --timeout 150 --timeout-method thread -rf
+  tail -3 "$O/tests.out"
+  step smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+  # dispatched forward tiles: 48 (C2), 128 (L=81 padded, L=100, L=128), 256 (C4 shape, small S)
+  for shp in "128 1000 38 38" "256 2000 81 81" "64 1000 100 100" "64 1000 128 128" "16 1024 1024 1024"; do
+    n=probe_$(echo $shp | tr ' ' _)
+    PROBE_BWD=1 step "$n" 300 python tools/repeat_probe.py $shp 30
+    cat "$O/$n.out"
+  done
+else
+  b c4_bench
+  b c4eval_bench --mode eval --no-cpu-baseline
+  b c2_bench --config c2 --no-cpu-baseline
+  b c2graph_bench --config c2 --graph --no-cpu-baseline
+  b c3_bench --config c3 --no-cpu-baseline
+  b c3graph_bench --config c3 --graph --no-cpu-baseline
+  b c5_1gpu_bench --config c5 --steps 3 --warmup 1 --no-cpu-baseline
+  for c in c1 c2 c3; do
+    for bl in cublaslt cublas; do
+      step ts_${c}_$bl 300 python tools/trainstep_profile.py --config $c --blas $bl
+      python -c "import json;d=json.load(open('$O/ts_${c}_$bl.out'));print('ts $c $bl',{k:d[k] for k in ('eager_ms','trainstep_ms','graph_ms')})"
+    done
+  done
+  TAG=r3_c4 bash tools/profile.sh || exit 1
+fi
+echo done
