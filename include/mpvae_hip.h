@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 5  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
-                              5: T rows padded to roundup(L, 4) floats */
+#define MPV_ABI_VERSION 6  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+                              5: T rows padded to roundup(L, 4) floats;
+                              6: mpv_linear (the VAE's Linear layers) */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -260,12 +261,46 @@ typedef struct mpv_reparam_bwd_args {
 
 int mpv_reparam_bwd(const mpv_reparam_bwd_args* args, void* stream);
 
+/* ------------------------------------------------- encoder/decoder MLPs a2/a4
+ * One fp32 matrix-core GEMM with a fused epilogue (linear.hip):
+ *   out[i * out_si + j] = act(alpha * (sum_r A(i, r) B(j, r) + bias[j]))
+ *   A(i, r) = a[i * a_si + r * a_sr] * a_scale, zeroed where a_mask (same
+ *             strides, optional) is not > 0 (the ReLU backward);
+ *   B(j, r) = b[j * b_sj + r * b_sr], or 1 for j == ones_col, whose output
+ *             goes to out_col[i] instead (the bias gradient; ones_col must be
+ *             N - 1, or -1 for none).
+ * act = ReLU when relu != 0 (NaN passes, as torch.relu).  Replaces nn.Linear
+ * (+ F.relu, + the `* scale_coeff` of mpvae.py:54-55,63-64) in the forward
+ * and the three GEMMs of its backward (mpvae.py:11-38 layers, :51-84 uses).
+ * The reduction is split over workgroups when the output is small; the
+ * chunk partials (workspace, mpv_linear_workspace_bytes) are summed in a
+ * fixed order, so results are deterministic. */
+typedef struct mpv_linear_args {
+  int64_t M, N, R;
+  const float* a;
+  int64_t a_si, a_sr;
+  const float* a_mask;
+  float a_scale;
+  const float* b;
+  int64_t b_sj, b_sr;
+  int64_t ones_col;
+  const float* bias; /* (N) or NULL */
+  float alpha;
+  int relu;
+  float* out;
+  int64_t out_si;
+  float* out_col;    /* (M), with ones_col */
+} mpv_linear_args;
+
+size_t mpv_linear_workspace_bytes(int64_t M, int64_t N, int64_t R);
+int mpv_linear(const mpv_linear_args* args, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------ measurement */
 /* When enabled, every kernel launch of the library is bracketed by a pair of
  * HIP events on the launch stream (bench.py's per-kernel roofline timing).
  * Kernel names: noise_philox, probit_fwd, fwd_combine, finalize, bwd_coef,
  * bwd_elem, dR_gemm, sum_slabs, convert, bstat_combine, reparam_fwd,
- * reparam_bwd, kl_bwd.  Query synchronises the recorded events. */
+ * reparam_bwd, kl_bwd, linear.  Query synchronises the recorded events. */
 int mpv_timing_enable(int on);
 int mpv_timing_reset(void);
 int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms);

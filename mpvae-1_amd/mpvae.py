@@ -10,9 +10,9 @@ Same public names, signatures, parameter names, shapes and dtypes:
 
 Put ``mpvae-1_amd/`` on ``sys.path`` and ``from mpvae import VAE, compute_loss``
 works unchanged in the reference's training loop (fairsoft_train.py:57-146).
-The arithmetic runs in hand-written gfx950 kernels (libmpvae_hip.so); the
-encoder/decoder MLPs stay ``nn.Linear`` (hipBLASLt), as SURVEY.md section 8(a)
-rows a2/a4 prescribe.
+The arithmetic runs in hand-written gfx950 kernels (libmpvae_hip.so),
+the encoder/decoder Linear layers included (``nn.Linear`` modules hold the
+parameters; their GEMMs run in mpv_linear, see ``mpvae_linear``).
 
 Build-only knobs read from ``args`` (defaults reproduce the reference):
   mpvae_noise  "torch_cpu" (default): draw the probit noise from torch's CPU
@@ -29,6 +29,10 @@ Build-only knobs read from ``args`` (defaults reproduce the reference):
                "f32": exact fp32 matrix-core GEMMs.
   mpvae_shard  True: shard the n_sample axis over the default
                torch.distributed group (mpvae_dist.py); default False.
+  mpvae_linear "hip" (default): the encoder / decoder Linear layers (with
+               their ReLU and scale_coeff) on the fp32 matrix cores
+               (mpvae_linear.py, csrc/linear.hip); "torch": nn.Linear
+               (hipBLASLt / rocBLAS), for A/B.
 """
 import numpy as np
 import torch
@@ -37,6 +41,7 @@ import torch.nn.functional as F
 
 import mpvae_hip
 import mpvae_dist
+import mpvae_linear
 from mpvae_ops import ElboConfig, FusedReparam, ProbitELBO, SingleReparam
 
 __all__ = ["VAE", "compute_loss"]
@@ -80,23 +85,38 @@ class VAE(nn.Module):
         assert self.fd1 is self.fd_x1 and self.fd2 is self.fd_x2
         self.dropout = nn.Dropout(p=args.keep_prob)   # keep_prob is the DROP rate (mpvae.py:38)
         self.scale_coeff = args.scale_coeff
+        self.linear_backend = getattr(args, "mpvae_linear", "hip")
+        if self.linear_backend not in ("hip", "torch"):
+            raise ValueError(f"mpvae_linear must be 'hip' or 'torch', got {self.linear_backend!r}")
         self.register_parameter("r_sqrt_sigma", _init_r_sqrt_sigma(args))
         # eps ~ N(0,1) like torch.randn_like (mpvae.py:68,73); replaceable for tests
         self.reparam_noise = torch.randn_like
 
+    # -- one Linear layer: act(alpha * layer(x)), act = ReLU if `relu`
+    def _lin(self, layer, x, relu=False, alpha=1.0):
+        if self.linear_backend == "hip":
+            return mpvae_linear.linear(x, layer, relu, alpha)
+        y = layer(x)
+        if relu:
+            return F.relu(y)
+        return y * alpha if alpha != 1.0 else y
+
     # -- encoders (mpvae.py:51-64)
     def _mlp(self, x, layers):
         for lin in layers:
-            x = self.dropout(F.relu(lin(x)))
+            x = self.dropout(self._lin(lin, x, relu=True))
         return x
 
+    def _heads(self, h, mu, logvar):
+        return (self._lin(mu, h, alpha=self.scale_coeff),
+                self._lin(logvar, h, alpha=self.scale_coeff))
+
     def label_encode(self, x):
-        h = self._mlp(x, (self.fe1, self.fe2))
-        return self.fe_mu(h) * self.scale_coeff, self.fe_logvar(h) * self.scale_coeff
+        return self._heads(self._mlp(x, (self.fe1, self.fe2)), self.fe_mu, self.fe_logvar)
 
     def feat_encode(self, x):
-        h = self._mlp(x, (self.fx1, self.fx2, self.fx3))
-        return self.fx_mu(h) * self.scale_coeff, self.fx_logvar(h) * self.scale_coeff
+        return self._heads(self._mlp(x, (self.fx1, self.fx2, self.fx3)), self.fx_mu,
+                           self.fx_logvar)
 
     # -- reparameterisation (mpvae.py:66-74), one encoder at a time
     def label_reparameterize(self, mu, logvar):
@@ -107,7 +127,8 @@ class VAE(nn.Module):
 
     # -- decoders (mpvae.py:76-84); fd1/fd2 are fd_x1/fd_x2
     def _decode(self, z, head):
-        return head(F.relu(self.fd_x2(F.relu(self.fd_x1(z)))))
+        h = self._lin(self.fd_x2, self._lin(self.fd_x1, z, relu=True), relu=True)
+        return self._lin(head, h)
 
     def label_decode(self, z):
         return self._decode(z, self.label_mp_mu)

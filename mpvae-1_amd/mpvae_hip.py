@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -90,6 +90,16 @@ class LabelTable(ctypes.Structure):
 FAIR_L1, FAIR_L2 = 1, 2
 
 
+class LinearArgs(ctypes.Structure):
+    """mpv_linear_args: one fp32 matrix-core GEMM with a fused epilogue (linear.hip)."""
+    _fields_ = [("M", ctypes.c_int64), ("N", ctypes.c_int64), ("R", ctypes.c_int64),
+                ("a", vp), ("a_si", ctypes.c_int64), ("a_sr", ctypes.c_int64), ("a_mask", vp),
+                ("a_scale", ctypes.c_float), ("b", vp), ("b_sj", ctypes.c_int64),
+                ("b_sr", ctypes.c_int64), ("ones_col", ctypes.c_int64), ("bias", vp),
+                ("alpha", ctypes.c_float), ("relu", ctypes.c_int), ("out", vp),
+                ("out_si", ctypes.c_int64), ("out_col", vp)]
+
+
 class FairArgs(ctypes.Structure):
     _fields_ = [("label_z", vp), ("feat_z", vp), ("w", vp), ("order", vp), ("goff", vp),
                 ("gid", vp), ("B", ctypes.c_int64), ("L", ctypes.c_int64), ("T", ctypes.c_int64),
@@ -123,6 +133,9 @@ SIGNATURES = {
     "mpv_kl_bwd": (ctypes.c_int, [ctypes.POINTER(KlBwdArgs), vp]),
     "mpv_reparam_fwd": (ctypes.c_int, [ctypes.POINTER(ReparamArgs), vp]),
     "mpv_reparam_bwd": (ctypes.c_int, [ctypes.POINTER(ReparamBwdArgs), vp]),
+    "mpv_linear_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64,
+                                                     ctypes.c_int64]),
+    "mpv_linear": (ctypes.c_int, [ctypes.POINTER(LinearArgs), vp, ctypes.c_size_t, vp]),
     "mpv_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "mpv_timing_reset": (ctypes.c_int, []),
     "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
@@ -188,7 +201,7 @@ def require_gpu(*tensors):
 
 KERNELS = ["noise_philox", "split", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
            "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
-           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics"]
+           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics", "linear"]
 
 
 def kernel_times():

@@ -1,0 +1,86 @@
+"""The VAE's Linear layers on the fp32 matrix cores (csrc/linear.hip).
+
+``linear(x, layer, relu=False, alpha=1.0)`` computes
+``act(alpha * (x @ layer.weight.T + layer.bias))`` -- nn.Linear, the F.relu
+after it (reference mpvae.py:53,58-62,78-84) and the ``* scale_coeff`` of the
+mu / logvar heads (:54-55,63-64) in one launch pair -- and its backward
+(d x, d W, d b, the ReLU mask and the scale folded into the GEMM operand
+loads) in two.  The parameters stay the reference's ``nn.Linear`` modules, so
+state_dict, optimiser and initialisation are unchanged.
+
+Why not nn.Linear: at the reference's batch sizes (32-512 rows) hipBLASLt tiles
+these GEMMs into a handful of workgroups that walk K ~ 1000 on one CU each
+(65-155 us per GEMM at C3, ~45 % of the drop-in training step,
+profiles/r03_c3_trainstep.json); mpv_linear splits the reduction until the
+launch fills the chip and sums the chunks in a fixed order (deterministic).
+"""
+import ctypes
+
+import torch
+
+import mpvae_hip as H
+
+
+def _launch(M, N, R, a, a_si, a_sr, b, b_sj, b_sr, out, out_si, *, a_mask=None, a_scale=1.0,
+            ones_col=-1, out_col=None, bias=None, alpha=1.0, relu=False):
+    lib = H.load_library()
+    args = H.LinearArgs(M=M, N=N, R=R, a=H.ptr(a), a_si=a_si, a_sr=a_sr, a_mask=H.ptr(a_mask),
+                        a_scale=a_scale, b=H.ptr(b), b_sj=b_sj, b_sr=b_sr, ones_col=ones_col,
+                        bias=H.ptr(bias), alpha=alpha, relu=int(bool(relu)), out=H.ptr(out),
+                        out_si=out_si, out_col=H.ptr(out_col))
+    nbytes = lib.mpv_linear_workspace_bytes(M, N, R)
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=out.device)
+    H.check(lib.mpv_linear(ctypes.byref(args), H.ptr(ws), nbytes, H.stream_of(out.device)),
+            "mpv_linear")
+
+
+def _rows(x):
+    """x with unit column stride (row stride free), as the kernels address it."""
+    return x if x.stride(1) == 1 else x.contiguous()
+
+
+class HipLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, alpha):
+        H.require_gpu(x, weight, bias)
+        if x.dtype != torch.float32 or weight.dtype != torch.float32:
+            raise TypeError("mpv_linear computes in fp32 (the reference's nn.Linear dtype)")
+        if x.dim() != 2:
+            raise ValueError(f"mpv_linear takes (batch, features) inputs, got {tuple(x.shape)}")
+        x = _rows(x)
+        w = weight.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        if w.shape[1] != K:
+            raise ValueError(f"mat1 and mat2 shapes cannot be multiplied ({M}x{K} and "
+                             f"{w.shape[1]}x{N})")
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        _launch(M, N, K, x, x.stride(0), 1, w, K, 1, y, N,
+                bias=None if bias is None else bias.contiguous(), alpha=alpha, relu=relu)
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.alpha, ctx.has_bias = alpha, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        gy = gy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            # dx[m, k] = sum_n g[m, n] W[n, k],  g = alpha * dy * (y > 0)
+            gx = torch.empty((M, K), dtype=torch.float32, device=x.device)
+            _launch(M, K, N, gy, N, 1, w, 1, K, gx, K, a_mask=y, a_scale=ctx.alpha)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # dW[n, k] = sum_m g[m, n] x[m, k]; db[n] = sum_m g[m, n] (ones column)
+            gw = torch.empty((N, K), dtype=torch.float32, device=x.device)
+            gb = torch.empty((N,), dtype=torch.float32, device=x.device) if ctx.has_bias else None
+            _launch(N, K + (1 if ctx.has_bias else 0), M, gy, 1, N, x, 1, x.stride(0), gw, K,
+                    a_mask=y, a_scale=ctx.alpha, ones_col=K if ctx.has_bias else -1, out_col=gb)
+        return gx, gw, gb, None, None
+
+
+def linear(x, layer, relu=False, alpha=1.0):
+    """act(alpha * layer(x)) on the matrix cores, act = ReLU if `relu`."""
+    return HipLinear.apply(x, layer.weight, layer.bias, bool(relu), float(alpha))

@@ -76,12 +76,16 @@ def _has_finite_grad(model):  # fairsoft_utils.py:28-41
 
 def _train_steps(use_ours, steps=3, feature_dim=30, label_dim=12, z_dim=12, latent_dim=8,
                  batch=16, n_train_sample=32, nll_coeff=0.5, c_coeff=10.0, lr=1e-3,
-                 trainstep=False):
+                 trainstep=False, linear="torch"):
     """The live loop body of fairsoft_train.py:45-146 (penalty-free): forward ->
     compute_loss -> backward -> clip 10 -> finite gate -> Adam step.
-    trainstep: ours through mpvae_step.TrainStep (fused Adam, device gate)."""
+    trainstep: ours through mpvae_step.TrainStep (fused Adam, device gate).
+    linear: our VAE's Linear backend.  The reference-tracking tests keep
+    nn.Linear on both sides, so they compare the ELBO path and the step logic;
+    mpv_linear is compared on its own (test_gpu_linear.py and below)."""
     args = _args(feature_dim=feature_dim, label_dim=label_dim, z_dim=z_dim, latent_dim=latent_dim,
-                 n_train_sample=n_train_sample, nll_coeff=nll_coeff, c_coeff=c_coeff)
+                 n_train_sample=n_train_sample, nll_coeff=nll_coeff, c_coeff=c_coeff,
+                 mpvae_linear=linear)
     model = _seeded_model(args, seed=7).to(DEV).train()
     opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-5, fused=trainstep)
     if trainstep:
@@ -164,6 +168,33 @@ def test_train_step_device_gate_tracks_reference_loop():
     np.testing.assert_allclose(l1, l2, rtol=1e-4)
     for k in p1:
         torch.testing.assert_close(p1[k], p2[k], rtol=1e-3, atol=1e-5, msg=k)
+
+
+def test_train_step_hip_linear_tracks_torch_linear():
+    """The drop-in step at C1's shapes with the Linear layers on mpv_linear
+    against nn.Linear, 4 Adam steps.  Adam's first steps move every parameter
+    by +-lr (m / sqrt(v) = sign(g)), so an element whose gradient sits at the
+    rounding level of two fp32 GEMM orders (or behind a ReLU flip) may move
+    the other way: the check is that losses agree, that almost no element
+    differs and that none differs by more than those sign flips allow."""
+    cfg = dict(feature_dim=1000, label_dim=38, z_dim=38, latent_dim=50, batch=32,
+               n_train_sample=10, nll_coeff=0.5, c_coeff=10.0, lr=7.5e-4, steps=4)
+    l1, p1 = _train_steps(True, trainstep=True, linear="hip", **cfg)
+    l2, p2 = _train_steps(True, trainstep=True, linear="torch", **cfg)
+    from tolerances import record
+    fracs, dmax = {}, {}
+    for k in p1:
+        d = (p1[k].double() - p2[k].double()).abs()
+        fracs[k] = float((d > 1e-5 + 1e-3 * p2[k].double().abs()).double().mean())
+        dmax[k] = float(d.max())
+    record("trainstep_hip_vs_torch_linear_frac", {"loss": max(abs(a / b - 1) for a, b in zip(l1, l2)),
+                                                  **{"frac_" + k: v for k, v in fracs.items()}})
+    record("trainstep_hip_vs_torch_linear_dmax", {"dmax_" + k: v for k, v in dmax.items()})
+    np.testing.assert_allclose(l1, l2, rtol=1e-4)
+    for k in p1:
+        assert fracs[k] < 2e-3, (k, fracs[k])
+        # |Adam update| <= ~3 lr per step even for sign-flipped moments
+        assert dmax[k] <= 4 * cfg["lr"] * cfg["steps"], (k, dmax[k])
 
 
 def test_train_step_skips_nonfinite_update_on_device():

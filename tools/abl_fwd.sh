@@ -10,7 +10,7 @@ while [ $# -gt 1 ]; do
   ( /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$R/include" -Icsrc $f \
       -c csrc/probit_fwd.hip -o "$R/abl/$n/probit_fwd.o" 2>/dev/null &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined \
-      -o "$R/abl/$n/libmpvae_hip.so" "$R/abl/$n/probit_fwd.o" build/probit_bwd.o build/util.o \
+      -o "$R/abl/$n/libmpvae_hip.so" "$R/abl/$n/probit_fwd.o" build/probit_bwd.o build/util.o build/linear.o \
       build/fairness.o && echo "built $n" ) &
 done
 wait

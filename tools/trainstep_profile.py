@@ -33,12 +33,12 @@ CONFIGS = {"c1": (1000, 38, 38, 50, 32, 10, 0.5, 10.0, 7.5e-4),
            "c3": (1000, 81, 81, 50, 256, 2000, 0.1, 200.0, 7.5e-4)}
 
 
-def build(cfg, dev, fused):
+def build(cfg, dev, fused, linear="hip"):
     F_, L, z, d, B, S, nllc, cc, lr = CONFIGS[cfg]
     args = argparse.Namespace(feature_dim=F_, latent_dim=d, label_dim=L, z_dim=z, keep_prob=0.5,
                               scale_coeff=1.0, residue_sigma="", n_train_sample=S,
                               n_test_sample=S, mode="train", nll_coeff=nllc, c_coeff=cc,
-                              mpvae_noise="philox",
+                              mpvae_noise="philox", mpvae_linear=linear,
                               mpvae_seed=torch.tensor([77], dtype=torch.int64, device=dev))
     torch.manual_seed(0)
     np.random.seed(0)
@@ -90,12 +90,14 @@ def main():
     # torch's BLAS backend for the nn.Linear GEMMs: hipBLASLt (torch's default on
     # MI355X) or rocBLAS ("cublas" in torch's naming)
     ap.add_argument("--blas", default=None, choices=["cublaslt", "cublas"])
+    # the VAE's Linear layers: mpv_linear ("hip", the default) or nn.Linear
+    ap.add_argument("--linear", default="hip", choices=["hip", "torch"])
     cli = ap.parse_args()
     dev = torch.device("cuda", 0)
     if cli.blas:
         torch.backends.cuda.preferred_blas_library(cli.blas)
 
-    args, model, opt, label, feat = build(cli.config, dev, fused=False)
+    args, model, opt, label, feat = build(cli.config, dev, fused=False, linear=cli.linear)
     for _ in range(3):
         eager_step(model, opt, args, label, feat)
     eager_ms = timed(lambda: eager_step(model, opt, args, label, feat), cli.steps)
@@ -108,7 +110,7 @@ def main():
         acc += [ev[i].elapsed_time(ev[i + 1]) for i in range(5)]
     phases = {n: round(v / cli.steps, 4) for n, v in zip(names, acc)}
 
-    args, model, opt, label, feat = build(cli.config, dev, fused=True)
+    args, model, opt, label, feat = build(cli.config, dev, fused=True, linear=cli.linear)
     ts = mpvae_step.TrainStep(model, opt, args)
     for _ in range(3):
         ts(label, feat)
@@ -139,7 +141,7 @@ def main():
         kernels = {"error": repr(e)[:300]}
 
     F_, L, z, d, B, S, nllc, cc, lr = CONFIGS[cli.config]
-    print(json.dumps({"blas": str(torch.backends.cuda.preferred_blas_library()),
+    print(json.dumps({"blas": str(torch.backends.cuda.preferred_blas_library()), "linear": cli.linear,
                       "config": {"name": cli.config, "feature_dim": F_, "label_dim": L, "z_dim": z,
                                  "latent_dim": d, "batch": B, "n_train_sample": S,
                                  "nll_coeff": nllc, "c_coeff": cc, "lr": lr},
