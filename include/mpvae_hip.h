@@ -295,6 +295,12 @@ typedef struct mpv_linear_args {
 size_t mpv_linear_workspace_bytes(int64_t M, int64_t N, int64_t R);
 int mpv_linear(const mpv_linear_args* args, void* workspace, size_t workspace_bytes, void* stream);
 
+/* n (1..2) independent mpv_linear problems in one launch pair (a layer's dx
+ * and dW + db); the workspace is the sum of the problems' own, in order. */
+size_t mpv_linear_batch_workspace_bytes(const mpv_linear_args* args, int n);
+int mpv_linear_batch(const mpv_linear_args* args, int n, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 /* ------------------------------------------------------------ measurement */
 /* When enabled, every kernel launch of the library is bracketed by a pair of
  * HIP events on the launch stream (bench.py's per-kernel roofline timing).

@@ -136,6 +136,9 @@ SIGNATURES = {
     "mpv_linear_workspace_bytes": (ctypes.c_size_t, [ctypes.c_int64, ctypes.c_int64,
                                                      ctypes.c_int64]),
     "mpv_linear": (ctypes.c_int, [ctypes.POINTER(LinearArgs), vp, ctypes.c_size_t, vp]),
+    "mpv_linear_batch_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(LinearArgs), ctypes.c_int]),
+    "mpv_linear_batch": (ctypes.c_int, [ctypes.POINTER(LinearArgs), ctypes.c_int, vp,
+                                        ctypes.c_size_t, vp]),
     "mpv_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "mpv_timing_reset": (ctypes.c_int, []),
     "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),

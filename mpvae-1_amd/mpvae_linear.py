@@ -5,7 +5,7 @@
 after it (reference mpvae.py:53,58-62,78-84) and the ``* scale_coeff`` of the
 mu / logvar heads (:54-55,63-64) in one launch pair -- and its backward
 (d x, d W, d b, the ReLU mask and the scale folded into the GEMM operand
-loads) in two.  The parameters stay the reference's ``nn.Linear`` modules, so
+loads) in one more.  The parameters stay the reference's ``nn.Linear`` modules, so
 state_dict, optimiser and initialisation are unchanged.
 
 Why not nn.Linear: at the reference's batch sizes (32-512 rows) hipBLASLt tiles
@@ -21,16 +21,21 @@ import torch
 import mpvae_hip as H
 
 
-def _launch(M, N, R, a, a_si, a_sr, b, b_sj, b_sr, out, out_si, *, a_mask=None, a_scale=1.0,
-            ones_col=-1, out_col=None, bias=None, alpha=1.0, relu=False):
-    lib = H.load_library()
-    args = H.LinearArgs(M=M, N=N, R=R, a=H.ptr(a), a_si=a_si, a_sr=a_sr, a_mask=H.ptr(a_mask),
+def _problem(M, N, R, a, a_si, a_sr, b, b_sj, b_sr, out, out_si, *, a_mask=None, a_scale=1.0,
+             ones_col=-1, out_col=None, bias=None, alpha=1.0, relu=False):
+    return H.LinearArgs(M=M, N=N, R=R, a=H.ptr(a), a_si=a_si, a_sr=a_sr, a_mask=H.ptr(a_mask),
                         a_scale=a_scale, b=H.ptr(b), b_sj=b_sj, b_sr=b_sr, ones_col=ones_col,
                         bias=H.ptr(bias), alpha=alpha, relu=int(bool(relu)), out=H.ptr(out),
                         out_si=out_si, out_col=H.ptr(out_col))
-    nbytes = lib.mpv_linear_workspace_bytes(M, N, R)
-    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=out.device)
-    H.check(lib.mpv_linear(ctypes.byref(args), H.ptr(ws), nbytes, H.stream_of(out.device)),
+
+
+def _launch(device, *problems):
+    """One launch (pair) for 1-2 independent problems."""
+    lib = H.load_library()
+    arr = (H.LinearArgs * len(problems))(*problems)
+    nbytes = lib.mpv_linear_batch_workspace_bytes(arr, len(problems))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+    H.check(lib.mpv_linear_batch(arr, len(problems), H.ptr(ws), nbytes, H.stream_of(device)),
             "mpv_linear")
 
 
@@ -55,8 +60,9 @@ class HipLinear(torch.autograd.Function):
             raise ValueError(f"mat1 and mat2 shapes cannot be multiplied ({M}x{K} and "
                              f"{w.shape[1]}x{N})")
         y = torch.empty((M, N), dtype=torch.float32, device=x.device)
-        _launch(M, N, K, x, x.stride(0), 1, w, K, 1, y, N,
-                bias=None if bias is None else bias.contiguous(), alpha=alpha, relu=relu)
+        _launch(x.device, _problem(M, N, K, x, x.stride(0), 1, w, K, 1, y, N,
+                                   bias=None if bias is None else bias.contiguous(), alpha=alpha,
+                                   relu=relu))
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.alpha, ctx.has_bias = alpha, bias is not None
         return y
@@ -68,16 +74,21 @@ class HipLinear(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         gx = gw = gb = None
+        problems = []
         if ctx.needs_input_grad[0]:
             # dx[m, k] = sum_n g[m, n] W[n, k],  g = alpha * dy * (y > 0)
             gx = torch.empty((M, K), dtype=torch.float32, device=x.device)
-            _launch(M, K, N, gy, N, 1, w, 1, K, gx, K, a_mask=y, a_scale=ctx.alpha)
+            problems.append(_problem(M, K, N, gy, N, 1, w, 1, K, gx, K, a_mask=y,
+                                     a_scale=ctx.alpha))
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # dW[n, k] = sum_m g[m, n] x[m, k]; db[n] = sum_m g[m, n] (ones column)
             gw = torch.empty((N, K), dtype=torch.float32, device=x.device)
             gb = torch.empty((N,), dtype=torch.float32, device=x.device) if ctx.has_bias else None
-            _launch(N, K + (1 if ctx.has_bias else 0), M, gy, 1, N, x, 1, x.stride(0), gw, K,
-                    a_mask=y, a_scale=ctx.alpha, ones_col=K if ctx.has_bias else -1, out_col=gb)
+            problems.append(_problem(N, K + (1 if ctx.has_bias else 0), M, gy, 1, N, x, 1,
+                                     x.stride(0), gw, K, a_mask=y, a_scale=ctx.alpha,
+                                     ones_col=K if ctx.has_bias else -1, out_col=gb))
+        if problems:
+            _launch(x.device, *problems)  # dx and dW + db in one launch pair
         return gx, gw, gb, None, None
 
 

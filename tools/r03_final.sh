@@ -40,10 +40,15 @@ else
   b c3_bench --config c3 --no-cpu-baseline
   b c3graph_bench --config c3 --graph --no-cpu-baseline
   b c5_1gpu_bench --config c5 --steps 3 --warmup 1 --no-cpu-baseline
+  # the drop-in training step: Linear layers on mpv_linear (default), on
+  # nn.Linear with hipBLASLt (torch's default) and with rocBLAS
   for c in c1 c2 c3; do
-    for bl in cublaslt cublas; do
-      step ts_${c}_$bl 300 python tools/trainstep_profile.py --config $c --blas $bl
-      python -c "import json;d=json.load(open('$O/ts_${c}_$bl.out'));print('ts $c $bl',{k:d[k] for k in ('eager_ms','trainstep_ms','graph_ms')})"
+    for v in hip torch_cublaslt torch_cublas; do
+      lin=${v%%_*}; bl=${v#*_}; extra=""
+      [ "$lin" = torch ] && extra="--blas $bl"
+      step ts_${c}_$v 300 python tools/trainstep_profile.py --config $c --linear $lin $extra \
+        $([ $c = c2 ] && [ $lin = hip ] && echo --ops)
+      python -c "import json;d=json.load(open('$O/ts_${c}_$v.out'));print('ts $c $v',{k:d[k] for k in ('eager_ms','trainstep_ms','graph_ms')})"
     done
   done
   TAG=r3_c4 bash tools/profile.sh || exit 1

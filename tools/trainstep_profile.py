@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--blas", default=None, choices=["cublaslt", "cublas"])
     # the VAE's Linear layers: mpv_linear ("hip", the default) or nn.Linear
     ap.add_argument("--linear", default="hip", choices=["hip", "torch"])
+    # also list the aten ops of one eager TrainStep call (what issues the launches)
+    ap.add_argument("--ops", action="store_true")
     cli = ap.parse_args()
     dev = torch.device("cuda", 0)
     if cli.blas:
@@ -140,8 +142,22 @@ def main():
     except Exception as e:  # profiler unavailable: report why
         kernels = {"error": repr(e)[:300]}
 
+    ops = None
+    if cli.ops:
+        from torch.profiler import ProfilerActivity, profile
+        _, model2, opt2, _, _ = build(cli.config, dev, fused=True, linear=cli.linear)
+        ts2 = mpvae_step.TrainStep(model2, opt2, args)
+        ts2(label, feat)
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            ts2(label, feat)
+            torch.cuda.synchronize()
+        rows = [(e.key, e.count) for e in prof.key_averages() if e.key.startswith("aten::")]
+        rows.sort(key=lambda r: -r[1])
+        ops = rows[:40]
+
     F_, L, z, d, B, S, nllc, cc, lr = CONFIGS[cli.config]
-    print(json.dumps({"blas": str(torch.backends.cuda.preferred_blas_library()), "linear": cli.linear,
+    print(json.dumps({"aten_ops_per_eager_step": ops,"blas": str(torch.backends.cuda.preferred_blas_library()), "linear": cli.linear,
                       "config": {"name": cli.config, "feature_dim": F_, "label_dim": L, "z_dim": z,
                                  "latent_dim": d, "batch": B, "n_train_sample": S,
                                  "nll_coeff": nllc, "c_coeff": cc, "lr": lr},
