@@ -297,6 +297,33 @@ __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int
   }
 }
 
+// A small operand (r_sqrt_sigma at L, z <= 128): every workgroup takes max |x|
+// over the whole input itself (at most kSplitSmall elements, L2-resident) and
+// splits its own share of the planes: one launch instead of three, and the
+// same scale bits in every workgroup (the max is exact in any order).
+constexpr int64_t kSplitSmall = 16384;  // input elements
+
+template <typename T>
+__global__ __launch_bounds__(256) void split_small_kernel(const T* __restrict__ x, int rows,
+                                                         int cols, mpv_split16 out) {
+  __shared__ float red[16];
+  const int n = rows * cols;
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf((float)x[i]));
+  const float s = pow2_scale(block_reduce<true>(m, red));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = s;
+  const int cp = (int)(out.ld >> 1), np = (int)out.rows_pad * cp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+    const int r = i / cp, c = i - r * cp;
+    const float v = (r < rows && c < cols) ? (float)x[r * cols + c] : 0.0f;
+    uint16_t h, l;
+    split_f16(v, s, h, l);
+    const int64_t o = chunked_index(r, out.ld, c);
+    out.data[o] = h;
+    out.data[o + kLoOff] = l;
+  }
+}
+
 // Philox noise straight into 3xf16 planes: plane row r = b*S_local + s holds
 // the noise of (s, b) (same values as the fp32 (S, B, z) draw, rows reordered
 // so that the s rows of one batch row are contiguous for the GEMMs).
@@ -381,6 +408,9 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
                                                             int rows,
                                                             const uint64_t* __restrict__ seed_dev) {
   philox_key(seed_dev, k0, k1);
+  // the planes' constant scale (no launch of its own; the GEMMs that read it
+  // run after this kernel)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = kNoiseScale;
   const int cols = (int)(out.ld >> 1);
   const int r_end = min(rows, (int)(blockIdx.x + 1) * kNoiseRows);
   constexpr int CPT = kNoiseCols;
@@ -398,7 +428,6 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
   }
 }
 
-__global__ void set_scalar_kernel(float* p, float v) { *p = v; }
 
 static unsigned grid_for(int64_t n, int threads, int64_t cap = 65536) {
   int64_t g = cdiv(n, threads);
@@ -500,6 +529,17 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
   MPV_REQUIRE(rows <= out->rows_pad && cols <= out->ld / 2, "planes smaller than the input");
   MPV_REQUIRE(x_dtype == MPV_F32 || x_dtype == MPV_F64, "unsupported dtype %d", x_dtype);
   hipStream_t s = as_stream(stream);
+  const int64_t plane_elems = out->rows_pad * (out->ld / 2);
+  if (rows * cols <= kSplitSmall && plane_elems < (int64_t(1) << 31)) {
+    const dim3 g((unsigned)std::min<int64_t>(cdiv(plane_elems, 256 * 4), 256));
+    if (x_dtype == MPV_F64)
+      MPV_LAUNCH("split", split_small_kernel<double>, g, dim3(256), 0, s, (const double*)x,
+                 (int)rows, (int)cols, *out);
+    else
+      MPV_LAUNCH("split", split_small_kernel<float>, g, dim3(256), 0, s, (const float*)x,
+                 (int)rows, (int)cols, *out);
+    return check_launch("split_f16");
+  }
   float* bmax = reinterpret_cast<float*>(workspace);
   const int64_t n = rows * cols;
   const unsigned g = grid_for(n, 256, kMaxBlocks);
@@ -525,7 +565,6 @@ static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_
   const int64_t rows = shape->S_local * shape->B;
   MPV_REQUIRE(out->rows_pad >= rows && out->ld / 2 >= shape->z, "noise planes too small");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(set_scalar_kernel, dim3(1), dim3(1), 0, s, out->scale, kNoiseScale);
   MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
   const int64_t tpr = out->ld / 2 / kNoiseCols;  // threads per plane row
   const unsigned threads = tpr >= 256 ? 256 : (unsigned)(cdiv(tpr, 64) * 64);
