@@ -28,6 +28,9 @@ namespace mpv {
 
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
                      hipStream_t s);
+int launch_sum_slabs_pair(const float* in0, int64_t nslab0, int64_t n0, void* out0,
+                          int out0_dtype, const float* in1, int64_t nslab1, int64_t n1,
+                          void* out1, int out1_dtype, hipStream_t s);
 int launch_scale(const float* block_max, int n, float* scale, hipStream_t s);
 
 // Upper bounds used for the G scale (3xf16): for E = Phi(u)(1-1e-6)+0.5e-6,
@@ -1002,8 +1005,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   else
     MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false, false>), eg, dim3(256), 0, st, ep);
   if (int rc = check_launch("bwd_elem")) return rc;
-  if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
-    return rc;
+  if (!a->dR32) {
+    if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
+      return rc;
+  }
 
   if (a->dR32) {
     const int64_t blocks = (int64_t)pl.nLt * pl.nZt * pl.nKc;
@@ -1046,7 +1051,10 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       MPV_LAUNCH("dR_gemm", (dR_gemm_kernel<4, 4>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
     }
     if (int rc = check_launch("dR_gemm")) return rc;
-    if (int rc = launch_sum_slabs(slab, pl.nKc, (int64_t)L * z, a->dR32, MPV_F32, st)) return rc;
+    // the column partials (d fe_out, d fx_out) and the dR slabs in one launch
+    if (int rc = launch_sum_slabs_pair(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32,
+                                       slab, pl.nKc, (int64_t)L * z, a->dR32, MPV_F32, st))
+      return rc;
   }
   return MPV_OK;
 }

@@ -51,6 +51,7 @@ struct FwdParams {
 // Tuning constants of the product kernels (each measured; DESIGN.md section 3
 // lists the variants that lost and were removed):
 constexpr int kCombineThreads = 1024;  // fwd_combine: one block per batch row
+constexpr int kCombineFoldSlabs = 64;  // s-chunk partials fwd_combine sums itself, at most
 constexpr int kFwdWant = 2048;         // target workgroup count of the forward grid (s-chunking)
 constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
 
@@ -1073,9 +1074,23 @@ __global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restri
                                                          const float* __restrict__ rowpart,
                                                          float* __restrict__ rowstat,
                                                          float* __restrict__ bstat, int S, int B,
-                                                         int L, int nNt) {
+                                                         int L, int nNt,
+                                                         const float* __restrict__ colpart,
+                                                         float* __restrict__ colsum, int nSc) {
   __shared__ float red[32];
   const int b = blockIdx.x, tid = threadIdx.x;
+  // this row's column sums over the s-chunks (colpart != NULL: the workgroups
+  // of several s-chunks wrote partials), summed in chunk order
+  if (colpart != nullptr) {
+    const int64_t n = 2 * (int64_t)B * L;
+    for (int i = tid; i < 2 * L; i += blockDim.x) {
+      const int k = i / L, l = i - k * L;
+      const int64_t o = ((int64_t)k * B + b) * L + l;
+      float acc = 0.0f;
+      for (int sc = 0; sc < nSc; ++sc) acc += colpart[sc * n + o];
+      colsum[o] = acc;
+    }
+  }
   float np = 0.f, nn = 0.f;
   for (int l = tid; l < L; l += blockDim.x) {
     const float v = y[(int64_t)b * L + l];
@@ -1312,10 +1327,14 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   MPV_REQUIRE(blocks < (int64_t(1) << 31), "grid too large");
   launch_fwd(pl, a->gemm, dim3((unsigned)blocks), st, p);
   if (int rc = check_launch("probit_fwd")) return rc;
+  // few s-chunks: fwd_combine sums the column partials too (one launch less);
+  // many (small B, long S): the slab-sum kernel's split reduction
+  const bool fold = pl.nSc > 1 && pl.nSc <= kCombineFoldSlabs;
   MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(kCombineThreads), 0, st, a->y,
-             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt);
+             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt, fold ? p.colpart : nullptr,
+             a->colsum, pl.nSc);
   if (int rc = check_launch("fwd_combine")) return rc;
-  if (pl.nSc > 1) {
+  if (pl.nSc > 1 && !fold) {
     if (int rc = launch_sum_slabs(p.colpart, pl.nSc, 2 * shape->B * shape->L, a->colsum, MPV_F32, st))
       return rc;
   }

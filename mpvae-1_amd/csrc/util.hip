@@ -176,6 +176,60 @@ __global__ __launch_bounds__(1024) void sum_slabs_split_kernel(const float* __re
   }
 }
 
+// Two slab sums in one launch (the backward's column partials and its dR
+// slabs): workgroups [0, a.blocks) sum problem a, the rest problem b, each in
+// the layout and order of sum_slabs_kernel (plain: a thread per element, the
+// slabs in order) or sum_slabs_split_kernel (split: 64 columns per workgroup,
+// 16 slab groups, partials added in order), so results are the bits of the
+// separate launches.
+struct SlabSum {
+  const float* in;
+  int64_t nslab, n;
+  void* out;
+  int f64;     // out is double
+  int split;   // the split layout (few columns, many slabs)
+  int64_t blocks;
+};
+
+MPV_DEV void slab_store(const SlabSum& q, int64_t i, float v) {
+  if (q.f64)
+    reinterpret_cast<double*>(q.out)[i] = (double)v;
+  else
+    reinterpret_cast<float*>(q.out)[i] = v;
+}
+
+__global__ __launch_bounds__(1024) void sum_slabs_pair_kernel(SlabSum a, SlabSum b) {
+  __shared__ float part[16][65];
+  const bool second = (int64_t)blockIdx.x >= a.blocks;
+  const SlabSum q = second ? b : a;
+  const int64_t blk = second ? (int64_t)blockIdx.x - a.blocks : (int64_t)blockIdx.x;
+  if (q.split) {
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = blk * 64 + lane;
+    float acc = 0.0f;
+    if (i < q.n) {
+#pragma unroll 4
+      for (int64_t k = g; k < q.nslab; k += 16) acc += q.in[k * q.n + i];
+    }
+    part[g][lane] = acc;
+    __syncthreads();
+    if (g == 0 && i < q.n) {
+      float t = part[0][lane];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) t += part[j][lane];
+      slab_store(q, i, t);
+    }
+  } else {
+    const int64_t i = blk * 1024 + threadIdx.x;
+    if (i < q.n) {
+      float acc = 0.0f;
+#pragma unroll 8
+      for (int64_t k = 0; k < q.nslab; ++k) acc += q.in[k * q.n + i];
+      slab_store(q, i, acc);
+    }
+  }
+}
+
 // gathered (R,6,B) -> out (6,B)
 __global__ void bstat_combine_kernel(const float* __restrict__ g, int64_t R, int64_t B,
                                      float* __restrict__ out) {
@@ -656,6 +710,29 @@ namespace mpv {
 int launch_scale(const float* block_max, int n, float* scale, hipStream_t s) {
   MPV_LAUNCH("bwd_coef", scale_kernel, dim3(1), dim3(256), 0, s, block_max, n, scale);
   return check_launch("scale");
+}
+
+static SlabSum slab_problem(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype) {
+  SlabSum q;
+  q.in = in;
+  q.nslab = nslab;
+  q.n = n;
+  q.out = out;
+  q.f64 = out_dtype == MPV_F64;
+  q.split = nslab >= 64 && n <= 256 * 256;  // the rule of launch_sum_slabs
+  q.blocks = q.split ? cdiv(n, 64) : cdiv(n, 1024);
+  return q;
+}
+
+int launch_sum_slabs_pair(const float* in0, int64_t nslab0, int64_t n0, void* out0,
+                          int out0_dtype, const float* in1, int64_t nslab1, int64_t n1,
+                          void* out1, int out1_dtype, hipStream_t s) {
+  const SlabSum a = slab_problem(in0, nslab0, n0, out0, out0_dtype);
+  const SlabSum b = slab_problem(in1, nslab1, n1, out1, out1_dtype);
+  MPV_REQUIRE(a.blocks + b.blocks < (int64_t(1) << 31), "slab sums too large");
+  MPV_LAUNCH("sum_slabs", sum_slabs_pair_kernel, dim3((unsigned)(a.blocks + b.blocks)), dim3(1024),
+             0, s, a, b);
+  return check_launch("sum_slabs");
 }
 
 int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype,
