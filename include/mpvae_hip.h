@@ -97,8 +97,8 @@ enum mpv_gemm { MPV_GEMM_F16X3 = 0, MPV_GEMM_F32 = 1 };
 size_t mpv_split_workspace_bytes(void);
 
 /* Columns the 3xf16 noise planes of this shape need (z padded to the dR
- * GEMM's tile: 128 when L and z are both <= 128, else 256); the planes'
- * ld is twice this. */
+ * GEMM's tile: 64 when L and z are both <= 64, 128 when both are <= 128,
+ * else 256); the planes' ld is twice this. */
 int64_t mpv_noise_plane_cols(const mpv_shape* shape);
 
 /* x (rows, cols) fp32 / fp64 -> split planes.  Used for r_sqrt_sigma

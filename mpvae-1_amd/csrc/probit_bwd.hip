@@ -838,10 +838,20 @@ constexpr int kDr16Tile = 256;  // 3xf16 dR tile: 256 x 256, 8 waves of 128 x 64
 // noise planes are padded to 128 columns instead of 256
 constexpr int kDr16TileSmall = 128;
 
+// Both <= 64 (mirflickr 38, the fairsoft adult-like 25 x 10): a 64 x 64 tile
+// (4 waves of 32 x 32), planes padded to 64 columns: half the G-plane and
+// noise-plane bytes of the 128 tile at L = z = 38
+constexpr int kDr16TileTiny = 64;
+
+#ifndef MPV_DR_TINY_CPC
+#define MPV_DR_TINY_CPC 2
+#endif
 constexpr int kDrSmallChunksPerCu = 2;  // K chunks per CU for the 128 tile
+constexpr int kDrTinyChunksPerCu = MPV_DR_TINY_CPC;  // and for the 64 tile
 constexpr int64_t kDrMaxChunkRows = 131072;  // longest split-K chunk (sample rows)
 
 static int dr16_tile(int64_t L, int64_t z) {
+  if (L <= kDr16TileTiny && z <= kDr16TileTiny) return kDr16TileTiny;
   return (L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall : kDr16Tile;
 }
 
@@ -885,7 +895,9 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.rows_pad = (int)(cdiv(rows, kr) * kr);
   // split-K chunks: the 3xf16 kernel (1 workgroup per CU) gets one workgroup
   // per CU in a single wave of equal chunks; the fp32 kernel several per CU
-  int64_t kc = planes ? cdiv((dr_tile == kDr16Tile ? 1 : kDrSmallChunksPerCu) * (int64_t)num_cus(), tiles)
+  const int cpc = dr_tile == kDr16Tile ? 1 : (dr_tile == kDr16TileTiny ? kDrTinyChunksPerCu
+                                                                      : kDrSmallChunksPerCu);
+  int64_t kc = planes ? cdiv(cpc * (int64_t)num_cus(), tiles)
                       : cdiv(1536, tiles);
   // but no K chunk longer than kDrMaxChunkRows: one fp32 accumulator per output
   // over 4.2 M rows (C5 on one GPU: 256 tiles, so one chunk each) drifted 1e-4
@@ -1029,8 +1041,11 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
       dp.rows_per_chunk = pl.dr_rows_per_chunk;
       dp.rows_pad = pl.rows_pad;
       // 256 x 256 tile, 8 waves of 128 x 64, 2-stage ring (128 KB LDS)
-      static_assert(kDr16Tile == 256 && kDr16TileSmall == 128, "launch configs below");
-      if (pl.dr_tile == kDr16TileSmall)  // 128 x 128, 4 waves of 64 x 64, 2 x 32 KB stages
+      static_assert(kDr16Tile == 256 && kDr16TileSmall == 128 && kDr16TileTiny == 64,
+                    "launch configs below");
+      if (pl.dr_tile == kDr16TileTiny)  // 64 x 64, 4 waves of 32 x 32, 2 x 16 KB stages
+        MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 2, 2, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
+      else if (pl.dr_tile == kDr16TileSmall)  // 128 x 128, 4 waves of 64 x 64, 2 x 32 KB stages
         MPV_LAUNCH("dR_gemm", (dR16_kernel<2, 2, 4, 4, 2>), dim3((unsigned)blocks), dim3(256), 0, st, dp);
       else  // 256 x 256, two wave groups one phase apart (dR16s)
         MPV_LAUNCH("dR_gemm", (dR16s_kernel<2, 4, 8, 4>), dim3((unsigned)blocks), dim3(512), 0, st, dp);

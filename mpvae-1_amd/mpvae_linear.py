@@ -48,8 +48,12 @@ class HipLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu, alpha):
         H.require_gpu(x, weight, bias)
-        if x.dtype != torch.float32 or weight.dtype != torch.float32:
+        if x.dtype != torch.float32 or weight.dtype != torch.float32 or (
+                bias is not None and bias.dtype != torch.float32):
             raise TypeError("mpv_linear computes in fp32 (the reference's nn.Linear dtype)")
+        if weight.dim() != 2 or (bias is not None and bias.shape != (weight.shape[0],)):
+            raise ValueError(f"bad Linear parameters: weight {tuple(weight.shape)}, "
+                             f"bias {None if bias is None else tuple(bias.shape)}")
         if x.dim() != 2:
             raise ValueError(f"mpv_linear takes (batch, features) inputs, got {tuple(x.shape)}")
         x = _rows(x)

@@ -53,11 +53,13 @@ def test_abi_version_and_host_entry_points():
     assert lib.mpv_convert(None, 0, None, 0, 4, None) == 1
 
 
-@pytest.mark.parametrize("L,z,cols", [(38, 38, 128), (128, 5, 128), (2, 128, 128), (129, 5, 256),
+@pytest.mark.parametrize("L,z,cols", [(38, 38, 64), (64, 64, 64), (65, 38, 128), (38, 65, 128),
+                                      (128, 5, 128), (2, 128, 128), (129, 5, 256),
                                       (5, 129, 256), (1024, 1024, 1024), (100, 300, 512)])
 def test_noise_plane_cols_follow_the_dr_tile(L, z, cols):
-    """Noise planes are padded to whole dR tiles: 128 columns when L and z are
-    both <= 128 (the 128 x 128 tile), else 256 (probit_bwd.hip, dr16_tile)."""
+    """Noise planes are padded to whole dR tiles: 64 columns when L and z are
+    both <= 64, 128 when both are <= 128 (the 64 / 128 square tiles), else 256
+    (probit_bwd.hip, dr16_tile)."""
     lib = H.load_library()
     assert lib.mpv_noise_plane_cols(H.Shape(16, 16, 0, 2, L, z)) == cols
     assert lib.mpv_noise_plane_cols(H.Shape(0, 16, 0, 2, L, z)) == 0  # bad shape

@@ -24,7 +24,7 @@ import mpvae
 from golden_io import OUTS
 from oracle import probit_elbo as pe
 from test_gpu_parity import _against_oracle, _np
-from tolerances import FWD_RTOL, GRAD_RTOL, HEADLINE_GRAD_RTOL, record, rel_err
+from tolerances import FWD_RTOL, GRAD_RTOL, HEADLINE_GRAD_RTOL, params_track, record, rel_err
 from test_gpu_vae import _train_steps
 
 pytestmark = pytest.mark.gpu
@@ -42,8 +42,7 @@ def test_c1_dropin_training_loop_tracks_reference():
     errs.update({"param_" + k: rel_err(_np(p1[k]), _np(p2[k])) for k in p1})
     record("c1_dropin_loop", errs)
     np.testing.assert_allclose(l1, l2, rtol=1e-4)
-    for k in p1:
-        torch.testing.assert_close(p1[k], p2[k], rtol=1e-3, atol=1e-5, msg=k)
+    params_track("c1_dropin_loop", p1, p2, cfg["lr"], cfg["steps"])
 
 
 FULL = {  # (L, z, B, S, d, nll_coeff, c_coeff): bench.py CONFIGS

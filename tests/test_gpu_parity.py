@@ -108,7 +108,8 @@ def test_philox_noise_matches_oracle(S, B, z, s_off):
     # the 3xf16 planes hold the same numbers (to the split's 2^-22) and zero padding
     pl = HipShardBackend("f16x3").make_noise(shape, DEV, seed=0x1234ABCD5678, offset=0)
     v = _np(pl.value())
-    assert v.shape == (S * B, pl.cols) and pl.cols % 128 == 0 and pl.ld == 2 * pl.cols
+    assert v.shape == (S * B, pl.cols) and pl.ld == 2 * pl.cols
+    assert pl.cols == H.load_library().mpv_noise_plane_cols(shape) and pl.cols % 64 == 0
     # plane row b*S + s holds eps[s, b]
     np.testing.assert_allclose(v[:, :z].reshape(B, S, z).transpose(1, 0, 2), ref, atol=2e-5,
                                rtol=2e-5)
