@@ -109,7 +109,9 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
 
 /* mpv_noise_philox writing split planes directly: S_local*B rows, plane row
  * b*S_local + s = eps[s, b, :] (the s rows of one batch row contiguous, as the
- * GEMMs stream them); the same numbers as mpv_noise_philox. */
+ * GEMMs stream them); the same numbers as mpv_noise_philox.  Columns z ..
+ * roundup(z, 32) - 1 are written as zeros; columns past that (the dR tile's
+ * padding, mpv_noise_plane_cols) are not written. */
 int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
                          const mpv_split16* out, void* stream);
 

@@ -874,7 +874,10 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   const int64_t dr_tile = planes ? dr16_tile(L, z) : 128;  // dR output tile edge
   pl.dr_tile = (int)dr_tile;
   pl.ldg = cdiv(L, dr_tile) * dr_tile;
-  const int64_t Lc = planes ? pl.ldg : L;  // columns the element pass covers
+  // columns the element pass covers: with planes, L rounded up to the 32-wide
+  // K slices (zeros past L); the rest of the dR tile's padding is never
+  // written: in the dR GEMM it only meets output rows >= L, which are not stored
+  const int64_t Lc = planes ? std::min<int64_t>(pl.ldg, cdiv(L, 32) * 32) : L;
   pl.nLc = (int)cdiv(Lc, 1024);
   pl.TPR = (int)(Lc >= 1024 ? 256 : cdiv(Lc, 4));
   pl.RPI = 256 / pl.TPR;
@@ -1003,7 +1006,7 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.B = B;
   ep.L = L;
   ep.ldT = (int)t_cols(L);
-  ep.Lc = want_planes ? (int)pl.ldg : L;
+  ep.Lc = want_planes ? (int)std::min<int64_t>(pl.ldg, cdiv(L, 32) * 32) : L;
   ep.TPR = pl.TPR;
   ep.RPI = pl.RPI;
   ep.rows_per_chunk = pl.rows_per_chunk;

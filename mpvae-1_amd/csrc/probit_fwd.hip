@@ -964,6 +964,93 @@ MPV_DEV bool fwd_tile_soft(const FwdParams& p, int b, int n0, int nthreads) {
   return __builtin_amdgcn_readfirstlane(__syncthreads_or(my_soft)) != 0;
 }
 
+// The transposed 3xf16 tile with an even sample split (launch_fwd: 96 labels x
+// 128 samples for 48 < L <= 96: 8 waves of 48 labels x 32 samples), 2-stage
+// ring.  The waves of the second half issue the stage DMA at static priority 1
+// (the other half starts its MFMAs at the barrier).
+template <int WL, int WS, int TL, int TS, int NSTAGE>
+__global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
+  constexpr int NW = WL * WS;
+  constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
+  constexpr int STAGE = (BM + BN) * kRowB;
+  constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN) * 4];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cacc = red + RED;
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL, ws = wid / WL;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  const bool soft_any = fwd_tile_soft<BN>(p, b, n0, NW * 64);
+  constexpr int NWD = NW / 2;  // DMA-issuing waves: the prio-1 half
+  const bool dmaw = wid >= NW / 2;
+  Fwd16Dma<BM, BN, NWD> dma;
+  dma.init(p, t_begin, b, n0, wid % NWD, lane);
+  if (dmaw) {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+
+  int gs = 0;
+  // the second half of the waves loses every age arbitration on its SIMD;
+  // static priority (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TS];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
+      if (NSTAGE == 2)
+        wait_vmcnt<0>();
+      else
+        wait_vmcnt_dyn(min(dma.issued - (gs + 1), NSTAGE - 2) * dma.per_wave());
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      FragT<TL, TS> f;
+      if (dmaw) dma.issue(p, smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE, t_end, nK, b);
+      fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
+      fwd16t_mfma<TL, TS>(acc, f);
+    }
+    if (MPV_ABL & 1) {  // timing study: no epilogue
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < TL; ++m)
+#pragma unroll
+        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
+      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
+    } else {
+      __builtin_amdgcn_s_setprio(0);
+      fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                          soft_any);
+      // back to the K-loop priorities
+      if (wid >= NW / 2)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
+}
+
 // ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
 // The transposed 3xf16 tile for L > 48: (TL * 64) labels x 128 samples, 8
 // waves (4 label groups x 2 sample groups), 2-stage LDS-DMA ring, one
@@ -1195,12 +1282,13 @@ struct FwdPlan {
 static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   FwdPlan pl;
   // tile configurations: 0 = 48 labels (L <= 48), 1 = 96 labels (fp32 mode,
-  // L <= 96), 2 = 128 labels (transposed 3xf16 tile, or the fp32 64 x 64
-  // waves), 3 = 256 labels (3xf16, L > 128).  3xf16 with 48 < L <= 96 takes
-  // the 128 x 128 transposed tile in spite of its pad labels (C3, L = 81:
-  // forward 0.216 -> 0.167 ms against a 96-label tile)
+  // L <= 96; 3xf16: the transposed 96 x 128 tile), 2 = 128 labels (transposed
+  // 3xf16 tile, or the fp32 64 x 64 waves), 3 = 256 labels (3xf16, L > 128).
+  // (Round 2 measured the 3xf16 96-label tile of probit_fwd16, MFMA-layout
+  // accumulators, slower at C3 than the 128-label transposed tile; the
+  // transposed 96-label tile is the one used now.)
   const bool f16 = gemm == MPV_GEMM_F16X3;
-  pl.cfg = s->L <= 48 ? 0 : ((s->L <= 96 && !f16) ? 1 : ((f16 && s->L > 128) ? 3 : 2));
+  pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : ((f16 && s->L > 128) ? 3 : 2));
   pl.BM = 128;
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
@@ -1237,9 +1325,13 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
       case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
         MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3, 4>), grid, dim3(512), 0, st, p);
         break;
+      case 1:  // 96 labels x 128 samples (48 < L <= 96), 8 waves of 48 x 32, even split
+        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 3, 2, 2>), grid, dim3(512), 0, st, p);
+        break;
       default:
-        // 128 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
-        // (C3: forward 0.187 -> 0.181 ms against the even 64 / 64 split).  A
+        // 128 labels x 128 samples (96 < L <= 128), 8 waves, asymmetric 80 / 48
+        // sample split (C3 before the 96-label tile: forward 0.187 -> 0.181 ms
+        // against the even 64 / 64 split).  A
         // 4-wave version of this tile (64 x 64 per wave, two workgroups per CU)
         // ran 0.031 ms faster at C3 but was not repeatable: 10-13 % of its
         // launches at C3 differed in one label-branch row statistic of a

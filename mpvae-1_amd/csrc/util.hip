@@ -427,12 +427,20 @@ MPV_DEV void noise16_quad(int64_t e_row, int c0, int z, uint64_t offset, uint32_
 
 // Columns c_first, c_first + c_step, ... (CPT each, two 16-B stores) of
 // plane row r.
+// Plane columns the noise kernel writes: z rounded up to the GEMMs' 32-wide K
+// slices (zeros past z).  Columns beyond that (the dR tile's padding) are left
+// as they are: the forward GEMM never reads them, and in the dR GEMM they only
+// meet output columns >= z, which are not stored.
+__host__ __device__ inline int noise_written_cols(const mpv_split16& out, int z) {
+  return (int)min(out.ld >> 1, (int64_t)((z + 31) / 32 * 32));
+}
+
 template <int CPT>
 MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_off, uint32_t k0,
                          uint32_t k1, uint64_t offset, int r, int c_first, int c_step) {
   const int bb = r / S, ss = r - bb * S;
   const int64_t e_row = ((s_off + ss) * B + bb) * (int64_t)z;  // first global element of the row
-  const int cols = (int)(out.ld >> 1);
+  const int cols = noise_written_cols(out, z);
   for (int c0 = c_first; c0 < cols; c0 += c_step) {
     float v[CPT];
 #pragma unroll
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
   // the planes' constant scale (no launch of its own; the GEMMs that read it
   // run after this kernel)
   if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = kNoiseScale;
-  const int cols = (int)(out.ld >> 1);
+  const int cols = noise_written_cols(out, z);
   const int r_end = min(rows, (int)(blockIdx.x + 1) * kNoiseRows);
   constexpr int CPT = kNoiseCols;
   const int tpr = min((int)blockDim.x, cols / CPT);  // threads per row
@@ -620,7 +628,7 @@ static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_
   MPV_REQUIRE(out->rows_pad >= rows && out->ld / 2 >= shape->z, "noise planes too small");
   hipStream_t s = as_stream(stream);
   MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
-  const int64_t tpr = out->ld / 2 / kNoiseCols;  // threads per plane row
+  const int64_t tpr = noise_written_cols(*out, (int)shape->z) / kNoiseCols;  // threads per plane row
   const unsigned threads = tpr >= 256 ? 256 : (unsigned)(cdiv(tpr, 64) * 64);
   MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(rows, kNoiseRows)),
              dim3(threads), 0, s, *out, (int)shape->S_local, (int)shape->B, (int)shape->z,

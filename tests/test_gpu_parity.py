@@ -113,7 +113,9 @@ def test_philox_noise_matches_oracle(S, B, z, s_off):
     # plane row b*S + s holds eps[s, b]
     np.testing.assert_allclose(v[:, :z].reshape(B, S, z).transpose(1, 0, 2), ref, atol=2e-5,
                                rtol=2e-5)
-    assert not v[:, z:].any()
+    # zeros up to the 32-wide K slice the forward reads; the dR tile's padding
+    # beyond it is not written (it only meets output columns >= z)
+    assert not v[:, z:(z + 31) // 32 * 32].any()
 
 
 @pytest.mark.parametrize("gemm", ["f16x3", "f32"])
