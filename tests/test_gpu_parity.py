@@ -220,6 +220,13 @@ RANDOM_CASES = [
     (1030, 96, 2, 20, 8),        # L > 1024: two bwd column chunks
     (1024, 1000, 2, 300, 8),     # 256-label tiles: 3 sample tiles, ragged K
     (260, 1024, 3, 257, 8),      # 256-label tiles, pad labels in the last label tile
+    # tile boundaries of round 3: forward 48 / 96 / 128-label tiles, dR 64 / 128 tiles
+    (48, 64, 4, 150, 8),         # last L of the 48-label tile; 64 x 64 dR tile at its edge
+    (49, 65, 4, 150, 8),         # first L of the 96-label tile; z = 65: 128 dR tile
+    (64, 63, 5, 140, 8),         # 64 dR tile, z % 32 != 0 (unwritten plane padding)
+    (96, 96, 3, 129, 8),         # last L of the 96-label tile, one s past a tile
+    (97, 33, 3, 100, 8),         # first L of the 128-label tile; noise planes 128 wide
+    (25, 10, 6, 64, 8),          # fairsoft adult-like dims (SURVEY fixture F3)
     (4096, 4096, 1, 40, 8),      # C5 dims (16 label tiles, 128 K stages), S < one tile
 ]
 
