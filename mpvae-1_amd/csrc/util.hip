@@ -392,41 +392,6 @@ constexpr float kNoiseScale = 4096.0f;
 // the block several rows at once.
 constexpr int kNoiseRows = 16;  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
 constexpr int kNoiseCols = 8;   // plane columns per thread (4: 1.78 ms, 8: 1.69 ms at C4)
-// Normals of columns c0 .. c0+3 (c0 % 4 == 0) of the plane row whose first
-// global element is e_row; zero past z.
-MPV_DEV void noise16_quad(int64_t e_row, int c0, int z, uint64_t offset, uint32_t k0, uint32_t k1,
-                          float (&v)[4]) {
-  v[0] = v[1] = v[2] = v[3] = 0.0f;
-  // Element e draws normal e & 3 of Philox counter e >> 2.  The row's first
-  // element is at phase sh (0 whenever z % 4 == 0; uniform over the row), so
-  // columns c0..c0+3 take normals sh..sh+3 of counters (e_row + c0) >> 2 and
-  // the next one: one Philox call when aligned, two otherwise.
-  if (c0 < z) {
-    const int sh = (int)(e_row & 3);
-    const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
-    const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
-    float a[8];
-    box_muller(w.x, w.y, a[0], a[1]);
-    box_muller(w.z, w.w, a[2], a[3]);
-    if (sh == 0) {
-      v[0] = a[0], v[1] = a[1], v[2] = a[2], v[3] = a[3];
-    } else {
-      const uint64_t c2 = ctr + 1;
-      const u32x4 w2 = philox4x32_10(u32x4{(uint32_t)c2, (uint32_t)(c2 >> 32), 0u, 0u}, k0, k1);
-      box_muller(w2.x, w2.y, a[4], a[5]);
-      if (sh > 1) box_muller(w2.z, w2.w, a[6], a[7]);
-      if (sh == 1) v[0] = a[1], v[1] = a[2], v[2] = a[3], v[3] = a[4];
-      else if (sh == 2) v[0] = a[2], v[1] = a[3], v[2] = a[4], v[3] = a[5];
-      else v[0] = a[3], v[1] = a[4], v[2] = a[5], v[3] = a[6];
-    }
-#pragma unroll
-    for (int q = 1; q < 4; ++q)
-      if (c0 + q >= z) v[q] = 0.0f;  // padding columns of the last group
-  }
-}
-
-// Columns c_first, c_first + c_step, ... (CPT each, two 16-B stores) of
-// plane row r.
 // Plane columns the noise kernel writes: z rounded up to the GEMMs' 32-wide K
 // slices (zeros past z).  Columns beyond that (the dR tile's padding) are left
 // as they are: the forward GEMM never reads them, and in the dR GEMM they only
@@ -435,6 +400,58 @@ __host__ __device__ inline int noise_written_cols(const mpv_split16& out, int z)
   return (int)min(out.ld >> 1, (int64_t)((z + 31) / 32 * 32));
 }
 
+// Normals of columns c0 .. c0+7 (c0 % 8 == 0) of the plane row whose first
+// global element is e_row; zero past z.  Element e draws normal e & 3 of
+// Philox counter e >> 2; the row's first element is at phase sh (0 whenever
+// z % 4 == 0; uniform over the row), so the 8 columns take normals sh..sh+7
+// of two consecutive counters when aligned and of three otherwise (two
+// 4-column groups made four calls, round 2).
+MPV_DEV void noise16_oct(int64_t e_row, int c0, int z, uint64_t offset, uint32_t k0, uint32_t k1,
+                         float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = 0.0f;
+  if (c0 >= z) return;
+  const int sh = (int)(e_row & 3);
+  const uint64_t ctr = (uint64_t)((e_row + c0) >> 2) + offset;
+  if (sh == 0) {  // aligned rows (z % 4 == 0): two counters, no selects
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const uint64_t c = ctr + g;
+      const u32x4 w = philox4x32_10(u32x4{(uint32_t)c, (uint32_t)(c >> 32), 0u, 0u}, k0, k1);
+      box_muller(w.x, w.y, v[4 * g], v[4 * g + 1]);
+      box_muller(w.z, w.w, v[4 * g + 2], v[4 * g + 3]);
+    }
+#pragma unroll
+    for (int i = 1; i < 8; ++i)
+      if (c0 + i >= z) v[i] = 0.0f;  // padding columns of the last group
+    return;
+  }
+  float a[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) a[i] = 0.0f;
+  const u32x4 w0 = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+  if (sh == 1) box_muller(w0.x, w0.y, a[0], a[1]);
+  box_muller(w0.z, w0.w, a[2], a[3]);
+  const uint64_t c1 = ctr + 1;
+  const u32x4 w1 = philox4x32_10(u32x4{(uint32_t)c1, (uint32_t)(c1 >> 32), 0u, 0u}, k0, k1);
+  box_muller(w1.x, w1.y, a[4], a[5]);
+  box_muller(w1.z, w1.w, a[6], a[7]);
+  {
+    const uint64_t c2 = ctr + 2;
+    const u32x4 w2 = philox4x32_10(u32x4{(uint32_t)c2, (uint32_t)(c2 >> 32), 0u, 0u}, k0, k1);
+    box_muller(w2.x, w2.y, a[8], a[9]);
+    if (sh == 3) box_muller(w2.z, w2.w, a[10], a[11]);
+  }
+  // v[i] = a[sh + i], sh in 1..3 (uniform per row: selects, not a dynamic index)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float x = sh == 1 ? a[i + 1] : (sh == 2 ? a[i + 2] : a[i + 3]);
+    v[i] = c0 + i < z ? x : 0.0f;
+  }
+}
+
+// Columns c_first, c_first + c_step, ... (CPT each, two 16-B stores) of
+// plane row r.
 template <int CPT>
 MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_off, uint32_t k0,
                          uint32_t k1, uint64_t offset, int r, int c_first, int c_step) {
@@ -442,14 +459,9 @@ MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_
   const int64_t e_row = ((s_off + ss) * B + bb) * (int64_t)z;  // first global element of the row
   const int cols = noise_written_cols(out, z);
   for (int c0 = c_first; c0 < cols; c0 += c_step) {
+    static_assert(CPT == 8, "noise16_oct: 8 columns per thread");
     float v[CPT];
-#pragma unroll
-    for (int g = 0; g < CPT / 4; ++g) {
-      float q[4];
-      noise16_quad(e_row, c0 + 4 * g, z, offset, k0, k1, q);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[4 * g + i] = q[i];
-    }
+    noise16_oct(e_row, c0, z, offset, k0, k1, v);
     uint16_t h[CPT], l[CPT];
 #pragma unroll
     for (int q = 0; q < CPT; ++q) split_f16(v[q], kNoiseScale, h[q], l[q]);
