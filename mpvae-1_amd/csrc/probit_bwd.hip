@@ -365,6 +365,30 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
 // Wave w moves pieces w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E.
 // The global base address is the piece's first row (wave-uniform: it goes in
 // an SGPR pair); with RPP > 1 a lane's row within the piece is in its offset.
+// Timing study (MPV_ABL & 65536): the VALU a
+// dR16s producer would add if it made G from T itself, one group-0 wave's
+// share per 32-row stage: 32 rows x 256 G columns x 42.5 lane-instructions
+// (bwd_elem's measured count per label-sample) / 64 lanes / 4 waves = 1360
+// wave-instructions, as 170 x (6 fma + exp + log) on 4 independent chains.
+MPV_DEV void dr_producer_valu_study() {
+  float x0 = 1.0f, x1 = 1.1f, x2 = 1.2f, x3 = 1.3f;
+  const float c = 0.999f;
+#pragma unroll 1
+  for (int j = 0; j < 170; ++j) {
+    asm volatile(
+        "v_fma_f32 %0, %0, %4, %4\n\t"
+        "v_fma_f32 %1, %1, %4, %4\n\t"
+        "v_fma_f32 %2, %2, %4, %4\n\t"
+        "v_fma_f32 %3, %3, %4, %4\n\t"
+        "v_fma_f32 %0, %0, %4, %4\n\t"
+        "v_fma_f32 %1, %1, %4, %4\n\t"
+        "v_exp_f32 %2, %2\n\t"
+        "v_log_f32 %3, %3"
+        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
+        : "v"(c));
+  }
+}
+
 template <int PER_WAVE, int PIECES, int RPP>
 MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
                       const int (&dma_off)[PER_WAVE]) {
@@ -630,6 +654,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
     if ((i) + 1 < nst)                                                                        \
       drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
                                   rows, wn, l0, z0, lane_u, lane_h);                          \
+    if (MPV_ABL & 65536) dr_producer_valu_study();                                            \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
     lds_barrier();                                                                            \
     __builtin_amdgcn_s_setprio(1);                                                            \
