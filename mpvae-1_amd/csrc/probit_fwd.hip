@@ -1061,6 +1061,30 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
 // already done and waits at the barrier; here the DMA half has less MFMA
 // work, so its DMA issue hides under the other half's longer MFMA phase.
 // IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).
+// Timing study (MPV_ABL & 65536): the VALU an
+// in-kernel noise generator would add to the forward, one DMA wave's share
+// per 32-K stage: 128 samples x 32 normals x 26.8 lane-instructions
+// (noise_philox16's measured count per normal) / 64 lanes / 4 waves = 429
+// wave-instructions, as 54 x (6 fma + exp + log) on 4 register chains.
+MPV_DEV void fwd_noise_valu_study() {
+  float x0 = 1.0f, x1 = 1.1f, x2 = 1.2f, x3 = 1.3f;
+  const float c = 0.999f;
+#pragma unroll 1
+  for (int j = 0; j < 54; ++j) {
+    asm volatile(
+        "v_fma_f32 %0, %0, %4, %4\n\t"
+        "v_fma_f32 %1, %1, %4, %4\n\t"
+        "v_fma_f32 %2, %2, %4, %4\n\t"
+        "v_fma_f32 %3, %3, %4, %4\n\t"
+        "v_fma_f32 %0, %0, %4, %4\n\t"
+        "v_fma_f32 %1, %1, %4, %4\n\t"
+        "v_exp_f32 %2, %2\n\t"
+        "v_log_f32 %3, %3"
+        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
+        : "v"(c));
+  }
+}
+
 template <int TSW, bool IS_A, int TSA, int TSB, int TL>
 MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cacc,
                           const float* cols, Fwd16Dma<128, TL * 64, 4>& dma, bool dmaw, int b, int nt,
@@ -1080,9 +1104,11 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
       wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
-      if (dmaw)
+      if (dmaw) {
         dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
                   t_end, nK, b);
+        if (MPV_ABL & 65536) fwd_noise_valu_study();
+      }
       FragT<TL, TSW> f;
       fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
       fwd16t_mfma<TL, TSW>(acc, f);
