@@ -2,7 +2,7 @@
 # mpv_linear with the in-kernel split reduction: its tests, the VAE / step
 # tests, the train step at C1-C3 (hip) and one aten-op listing.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-O="$R/gpurun_out/${OUT:-lin4}"
+O="$R/gpurun_out/${OUT:-lin}"
 mkdir -p "$O"
 cd "$R"
 step() {
