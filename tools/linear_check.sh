@@ -1,5 +1,5 @@
 #!/bin/bash
-# mpv_linear with the in-kernel split reduction: its tests, the VAE / step
+# mpv_linear on one GPU box: its parity tests (errors recorded), the VAE / step
 # tests, the train step at C1-C3 (hip) and one aten-op listing.
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/${OUT:-lin}"
