@@ -1051,16 +1051,6 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
 }
 
-// ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
-// The transposed 3xf16 tile for L > 48: (TL * 64) labels x 128 samples, 8
-// waves (4 label groups x 2 sample groups), 2-stage LDS-DMA ring, one
-// workgroup per CU.  The 128 samples are split unevenly between the two waves
-// of each SIMD: waves 0-3 own TSA 16-sample blocks, waves 4-7 TSB (< TSA) and
-// stream every stage's DMA at static priority 1.  With an even split the DMA half
-// runs its 48 MFMAs after ~800 cycles of DMA issue while the other half is
-// already done and waits at the barrier; here the DMA half has less MFMA
-// work, so its DMA issue hides under the other half's longer MFMA phase.
-// IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).
 // Timing study (MPV_ABL & 65536): the VALU an
 // in-kernel noise generator would add to the forward, one DMA wave's share
 // per 32-K stage: 128 samples x 32 normals x 26.8 lane-instructions
@@ -1085,6 +1075,16 @@ MPV_DEV void fwd_noise_valu_study() {
   }
 }
 
+// ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
+// The transposed 3xf16 tile for L > 48: (TL * 64) labels x 128 samples, 8
+// waves (4 label groups x 2 sample groups), 2-stage LDS-DMA ring, one
+// workgroup per CU.  The 128 samples are split unevenly between the two waves
+// of each SIMD: waves 0-3 own TSA 16-sample blocks, waves 4-7 TSB (< TSA) and
+// stream every stage's DMA at static priority 1.  With an even split the DMA half
+// runs its 48 MFMAs after ~800 cycles of DMA issue while the other half is
+// already done and waits at the barrier; here the DMA half has less MFMA
+// work, so its DMA issue hides under the other half's longer MFMA phase.
+// IS_A: waves 0-3 (TSA blocks); else waves 4-7 (TSB blocks, DMA).
 template <int TSW, bool IS_A, int TSA, int TSB, int TL>
 MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cacc,
                           const float* cols, Fwd16Dma<128, TL * 64, 4>& dma, bool dmaw, int b, int nt,
