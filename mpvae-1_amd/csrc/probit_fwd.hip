@@ -756,7 +756,10 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   ecount *= kC0;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
-  // (unrolled by 2, 15 VGPRs spill; fully, 95)
+  // (round 2: unrolled by 2, 15 VGPRs spill; fully, 95.  Round 3's compiler
+  // unrolls fully without spilling, and the forward measures the same: C4
+  // 13.28 / 13.25 vs 13.33 / 13.20 ms, so the rotation's moves are not on the
+  // critical path)
 #pragma unroll 1
   for (int m = 0; m < TL; ++m) {
     f32x4 am[TS];
