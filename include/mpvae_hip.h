@@ -34,7 +34,8 @@ extern "C" {
 
 #define MPV_ABI_VERSION 6  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
                               5: T rows padded to roundup(L, 4) floats;
-                              6: mpv_linear (the VAE's Linear layers) */
+                              6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
+                                 dR64 and kl */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -183,6 +184,8 @@ typedef struct mpv_final_args {
 int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* args, void* stream);
 
 /* --------------------------------------------------------------- backward */
+struct mpv_kl_bwd_args;  /* below */
+
 typedef struct mpv_bwd_args {
   const float* y;
   const float* fe_out;
@@ -204,6 +207,9 @@ typedef struct mpv_bwd_args {
   float* dR32;                 /* (L,z) out fp32 d r_sqrt_sigma (this shard), or NULL */
   void* workspace;
   size_t workspace_bytes;
+  double* dR64;                /* (L,z) out fp64 d r_sqrt_sigma instead of dR32, for an fp64
+                                  r_sqrt_sigma with no cross-shard sum to follow; or NULL */
+  const struct mpv_kl_bwd_args* kl; /* run the KL backward (mpv_kl_bwd) in this call, or NULL */
 } mpv_bwd_args;
 
 size_t mpv_bwd_workspace_bytes(const mpv_shape* shape, int gemm);

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mpvae_hip.h"
+
 #define MPV_DEV __device__ __forceinline__
 
 namespace mpv {
@@ -381,6 +383,28 @@ MPV_DEV void block_reduce2(float& a, float& b, float* red) {
     rb = IS_MAX ? fmaxf(rb, red[16 + i]) : rb + red[16 + i];
   }
   a = ra, b = rb;
+}
+
+// d KL / d (mu, logvar) of mpvae.py:147-148, scaled by the upstream gradient
+// g = gscal[KL] + 1.1 * gscal[TOTAL], for elements i0, i0 + stride, ...
+// (mpv_kl_bwd's kernel, and the extra workgroups of the backward's bwd_coef).
+template <typename KlArgs>
+MPV_DEV void kl_bwd_range(const KlArgs& a, int64_t i0, int64_t stride) {
+  const int64_t n = a.B * a.d;
+  const float g = a.gscal[MPV_G_KL] + kKlWeight * a.gscal[MPV_G_TOTAL];
+  const float s = 0.5f * g / (float)a.B;
+  for (int64_t i = i0; i < n; i += stride) {
+    const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
+    const float dm = a.fx_mu[i] - a.fe_mu[i];
+    const float ex = expf(lvx);
+    const float den = ex + kKlEps;
+    const float r = expf(lve - lvx);
+    const float gm = s * 2.0f * dm / den;
+    a.g_fe_mu[i] = -gm;
+    a.g_fx_mu[i] = gm;
+    a.g_fe_logvar[i] = s * (r - 1.0f);
+    a.g_fx_logvar[i] = s * (1.0f - r - dm * dm * ex / (den * den));
+  }
 }
 
 // ---- 3xf16 split operands ---------------------------------------------------

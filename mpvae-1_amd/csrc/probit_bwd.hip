@@ -45,8 +45,13 @@ __global__ __launch_bounds__(1024) void bwd_coef_kernel(
     const float* __restrict__ y, const float* __restrict__ rowstat, const float* __restrict__ bstat,
     const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
     float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
-    float nll_coeff, float c_coeff, int live) {
+    float nll_coeff, float c_coeff, int live, mpv_kl_bwd_args kl, int kl_blocks) {
   __shared__ float red[32];
+  if ((int)blockIdx.x >= B) {  // the extra workgroups: the KL backward (mpv_bwd_args.kl)
+    kl_bwd_range(kl, (int64_t)(blockIdx.x - B) * blockDim.x + threadIdx.x,
+                 (int64_t)kl_blocks * blockDim.x);
+    return;
+  }
   const int b = blockIdx.x, tid = threadIdx.x;
   float np = 0.f, nn = 0.f, gi = 0.f;
   for (int l = tid; l < L; l += blockDim.x) {
@@ -972,7 +977,16 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
               a->gemm);
   const bool planes = a->gemm == MPV_GEMM_F16X3;
   const BwdPlan pl = plan_bwd(shape, a->gemm);
-  if (a->dR32) {
+  MPV_REQUIRE(!(a->dR32 && a->dR64), "dR32 or dR64, not both");
+  void* const dR_out = a->dR64 ? (void*)a->dR64 : (void*)a->dR32;
+  const int dR_dtype = a->dR64 ? MPV_F64 : MPV_F32;
+  if (a->kl) {
+    MPV_REQUIRE(a->kl->fe_mu && a->kl->fe_logvar && a->kl->fx_mu && a->kl->fx_logvar &&
+                    a->kl->gscal && a->kl->g_fe_mu && a->kl->g_fe_logvar && a->kl->g_fx_mu &&
+                    a->kl->g_fx_logvar && a->kl->B > 0 && a->kl->d > 0,
+                "bad kl arguments");
+  }
+  if (dR_out) {
     if (planes) {
       MPV_REQUIRE(a->eps16.data && a->eps16.scale, "eps16 planes are NULL");
       MPV_REQUIRE(a->eps16.ld >= 2 * (int64_t)pl.nZt * pl.dr_tile && a->eps16.ld % 64 == 0 &&
@@ -999,11 +1013,18 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
                                               pl.slab_bytes + pl.bound_bytes);
   const int64_t gld = 2 * pl.ldg;
   const int S = (int)shape->S_local, B = (int)shape->B, L = (int)shape->L, z = (int)shape->z;
-  const bool want_planes = planes && a->dR32 != nullptr;
+  const bool want_planes = planes && dR_out != nullptr;
 
-  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B), dim3(1024), 0, st, a->y, a->rowstat, a->bstat,
-             a->gscal, a->g_indiv, a->g_indiv_label, coef, want_planes ? gbound : nullptr, S, B, L,
-             (float)shape->S_total, a->nll_coeff, a->c_coeff, a->live);
+  mpv_kl_bwd_args kl{};
+  int kl_blocks = 0;
+  if (a->kl) {
+    kl = *a->kl;
+    kl_blocks = (int)std::min<int64_t>(cdiv(kl.B * kl.d, 1024), 256);
+  }
+  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B + kl_blocks), dim3(1024), 0, st, a->y, a->rowstat,
+             a->bstat, a->gscal, a->g_indiv, a->g_indiv_label, coef,
+             want_planes ? gbound : nullptr, S, B, L, (float)shape->S_total, a->nll_coeff,
+             a->c_coeff, a->live, kl, kl_blocks);
   if (int rc = check_launch("bwd_coef")) return rc;
   if (want_planes) {
     if (int rc = launch_scale(gbound, B, gscale, st)) return rc;
@@ -1045,12 +1066,12 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   else
     MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, false, false>), eg, dim3(256), 0, st, ep);
   if (int rc = check_launch("bwd_elem")) return rc;
-  if (!a->dR32) {
+  if (!dR_out) {
     if (int rc = launch_sum_slabs(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32, st))
       return rc;
   }
 
-  if (a->dR32) {
+  if (dR_out) {
     const int64_t blocks = (int64_t)pl.nLt * pl.nZt * pl.nKc;
     if (planes) {
       Dr16Params dp;
@@ -1096,7 +1117,7 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
     if (int rc = check_launch("dR_gemm")) return rc;
     // the column partials (d fe_out, d fx_out) and the dR slabs in one launch
     if (int rc = launch_sum_slabs_pair(colpart, pl.nSc, 2 * (int64_t)B * L, a->dfe_dfx, MPV_F32,
-                                       slab, pl.nKc, (int64_t)L * z, a->dR32, MPV_F32, st))
+                                       slab, pl.nKc, (int64_t)L * z, dR_out, dR_dtype, st))
       return rc;
   }
   return MPV_OK;

@@ -285,25 +285,9 @@ __global__ void reparam_bwd_kernel(mpv_reparam_bwd_args a) {
   glv[j] = g * ep[j] * 0.5f * expf(0.5f * lv[j]);
 }
 
-// d KL / d (mu, logvar) of mpvae.py:147-148, scaled by the upstream gradient
-// g = gscal[KL] + 1.1 * gscal[TOTAL].
+// d KL / d (mu, logvar) of mpvae.py:147-148 (kl_bwd_range, mpv_common.h).
 __global__ void kl_bwd_kernel(mpv_kl_bwd_args a) {
-  const int64_t n = a.B * a.d;
-  const float g = a.gscal[MPV_G_KL] + kKlWeight * a.gscal[MPV_G_TOTAL];
-  const float s = 0.5f * g / (float)a.B;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
-    const float dm = a.fx_mu[i] - a.fe_mu[i];
-    const float ex = expf(lvx);
-    const float den = ex + kKlEps;
-    const float r = expf(lve - lvx);
-    const float gm = s * 2.0f * dm / den;
-    a.g_fe_mu[i] = -gm;
-    a.g_fx_mu[i] = gm;
-    a.g_fe_logvar[i] = s * (r - 1.0f);
-    a.g_fx_logvar[i] = s * (1.0f - r - dm * dm * ex / (den * den));
-  }
+  kl_bwd_range(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 // --------------------------------------------------------- 3xf16 operands

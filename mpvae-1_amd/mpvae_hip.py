@@ -61,7 +61,8 @@ class BwdArgs(ctypes.Structure):
                 ("rowstat", vp), ("bstat", vp), ("gscal", vp), ("g_indiv", vp),
                 ("g_indiv_label", vp), ("nll_coeff", ctypes.c_float),
                 ("c_coeff", ctypes.c_float), ("live", ctypes.c_int), ("dfe_dfx", vp),
-                ("dR32", vp), ("workspace", vp), ("workspace_bytes", ctypes.c_size_t)]
+                ("dR32", vp), ("workspace", vp), ("workspace_bytes", ctypes.c_size_t),
+                ("dR64", vp), ("kl", vp)]
 
 
 class KlBwdArgs(ctypes.Structure):

@@ -11,6 +11,8 @@ only backend the product ever uses).
 ``FusedReparam`` is the reparameterisation of both encoders in one launch
 (mpvae.py:66-74).
 """
+import ctypes
+
 import torch
 
 import mpvae_hip as H
@@ -193,32 +195,55 @@ class HipShardBackend:
                 "mpv_probit_finalize")
         return (*scal, indiv, indiv_label)
 
-    def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR):
+    def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR,
+                       dR_dtype=torch.float32, kl=False):
+        """d fe_out, d fx_out and (want_dR) d r_sqrt_sigma of this shard.
+        dR_dtype float64: dR written in fp64 directly (no cross-shard sum may
+        follow: it is then not part of the packed fp32 buffer).  kl: the KL
+        backward runs in the same call (saved fe_mu ... fx_logvar)."""
         lib = H.load_library()
         dev = gscal.device
         B, L, z = shape.B, shape.L, shape.z
         n_fe = 2 * B * L
-        flat = torch.empty((n_fe + (L * z if want_dR else 0),), device=dev, dtype=torch.float32)
+        dR64 = None
+        if want_dR and dR_dtype == torch.float64:
+            dR64 = torch.empty((L, z), device=dev, dtype=torch.float64)
+        with_32 = want_dR and dR64 is None
+        flat = torch.empty((n_fe + (L * z if with_32 else 0),), device=dev, dtype=torch.float32)
         dfe_dfx = flat[:n_fe].view(2, B, L)
-        dR32 = flat[n_fe:].view(L, z) if want_dR else None
+        dR = flat[n_fe:].view(L, z) if with_32 else dR64
         nbytes = lib.mpv_bwd_workspace_bytes(shape, self.gemm)
         ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
         eps = saved["eps"]
         eps_ops = (None, eps.c()) if self.gemm == H.GEMM_F16X3 else (H.ptr(eps), H.Split16())
+        kl_outs, kl_ref = None, None
+        if kl:
+            kl_args, kl_outs = self._kl_args(saved["fe_mu"], saved["fe_logvar"], saved["fx_mu"],
+                                             saved["fx_logvar"], gscal)
+            kl_ref = ctypes.byref(kl_args)
         args = H.BwdArgs(H.ptr(saved["y"]), H.ptr(saved["fe_out"]), H.ptr(saved["fx_out"]),
                          self.gemm, *eps_ops, H.ptr(saved["T"]), H.ptr(saved["rowstat"]),
                          H.ptr(saved["bstat"]), H.ptr(gscal), H.ptr(g_I), H.ptr(g_IL),
-                         nll_coeff, c_coeff, live, H.ptr(dfe_dfx), H.ptr(dR32), H.ptr(ws), nbytes)
+                         nll_coeff, c_coeff, live, H.ptr(dfe_dfx),
+                         H.ptr(dR if with_32 else None), H.ptr(ws), nbytes, H.ptr(dR64),
+                         ctypes.cast(kl_ref, ctypes.c_void_p) if kl_ref is not None else None)
         H.check(lib.mpv_probit_bwd(shape, args, H.stream_of(dev)), "mpv_probit_bwd")
-        return flat, dfe_dfx, dR32
+        if kl:
+            return flat, dfe_dfx, dR, kl_outs
+        return flat, dfe_dfx, dR
 
-    def kl_backward(self, fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
+    @staticmethod
+    def _kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
         B, d = fe_mu.shape
         outs = [torch.empty_like(fe_mu) for _ in range(4)]
         args = H.KlBwdArgs(H.ptr(fe_mu), H.ptr(fe_logvar), H.ptr(fx_mu), H.ptr(fx_logvar), B, d,
                            H.ptr(gscal), *[H.ptr(o) for o in outs])
+        return args, outs  # outs: g_fe_mu, g_fe_logvar, g_fx_mu, g_fx_logvar
+
+    def kl_backward(self, fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
+        args, outs = self._kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal)
         H.check(H.load_library().mpv_kl_bwd(args, H.stream_of(fe_mu.device)), "mpv_kl_bwd")
-        return outs  # g_fe_mu, g_fe_logvar, g_fx_mu, g_fx_logvar
+        return outs
 
 
 class LocalExchange:
@@ -306,18 +331,31 @@ class ProbitELBO(torch.autograd.Function):
         g_I = None if g_I is None else g_I.to(torch.float32).contiguous()
         g_IL = None if g_IL is None else g_IL.to(torch.float32).contiguous()
         grads = [None] * 10
+        want_kl = need[2] or need[3] or need[5] or need[6]
+        gk = None
         if ctx.keep_T and (need[1] or need[4] or need[7]):
-            flat, dfe_dfx, dR32 = be.backward_local(shape, sv, gscal, live, g_I, g_IL,
-                                                    cfg.nll_coeff, cfg.c_coeff, need[7])
+            # one shard: dR straight in R's dtype and the KL backward in the
+            # same call (two launches fewer); sharded: the packed fp32 buffer
+            # is summed over the ranks first
+            local = getattr(cfg.exchange, "world", 1) == 1 and isinstance(cfg.exchange,
+                                                                         LocalExchange)
+            dR_dtype = ctx.r_dtype if local else torch.float32
+            res = be.backward_local(shape, sv, gscal, live, g_I, g_IL, cfg.nll_coeff,
+                                    cfg.c_coeff, need[7], dR_dtype=dR_dtype, kl=want_kl)
+            flat, dfe_dfx, dR = res[:3]
+            if want_kl:
+                gk = res[3]
             cfg.exchange.reduce_grads(flat)
             if need[1]:
                 grads[1] = dfe_dfx[0]
             if need[4]:
                 grads[4] = dfe_dfx[1]
             if need[7]:
-                grads[7] = be.from_f32(dR32, ctx.r_dtype)
-        if need[2] or need[3] or need[5] or need[6]:
-            gk = be.kl_backward(sv["fe_mu"], sv["fe_logvar"], sv["fx_mu"], sv["fx_logvar"], gscal)
+                grads[7] = dR if dR.dtype == ctx.r_dtype else be.from_f32(dR, ctx.r_dtype)
+        if want_kl:
+            if gk is None:
+                gk = be.kl_backward(sv["fe_mu"], sv["fe_logvar"], sv["fx_mu"], sv["fx_logvar"],
+                                    gscal)
             grads[2], grads[3], grads[5], grads[6] = gk
         ctx.saved = None
         return tuple(grads)

@@ -66,7 +66,22 @@ class OracleShardBackend:
                  c_x=(gs[4] + c_coeff * gs[0]) if livef(0, 4) else None)
         return g
 
-    def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR):
+    def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR,
+                       dR_dtype=torch.float32, kl=False):
+        """HipShardBackend.backward_local's contract: dR in dR_dtype (a
+        separate tensor when fp64), the KL gradients appended when kl."""
+        out = self._backward_local(shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff,
+                                   want_dR)
+        if want_dR and dR_dtype == torch.float64:
+            flat, dfe_dfx, dR = out
+            n = 2 * shape.B * shape.L
+            out = (flat[:n].clone(), dfe_dfx, dR.to(torch.float64))
+        if kl:
+            out = (*out, self.kl_backward(saved["fe_mu"], saved["fe_logvar"], saved["fx_mu"],
+                                          saved["fx_logvar"], gscal))
+        return out
+
+    def _backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR):
         g = self._g(gscal, live, nll_coeff, c_coeff)
         y = saved["y"].numpy()
         coef = pe.row_coefficients(saved["rowstat"].double().numpy(),
