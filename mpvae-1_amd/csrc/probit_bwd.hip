@@ -41,7 +41,11 @@ int launch_scale(const float* block_max, int n, float* scale, hipStream_t s);
 constexpr float kBoundDl = 4.5f, kBoundPos = 0.4f, kBoundNeg = 60.0f, kBoundInd = 0.4f;
 
 // --------------------------------------------------------------- coefficients
-__global__ __launch_bounds__(1024) void bwd_coef_kernel(
+// bwd_coef: one workgroup per batch row (512 or 256 threads: C2 -1.7 / +0 us,
+// C3 +-0 / +2 us, C4 +-0 / +3 us; round 3, same box)
+constexpr int kCoefThreads = 1024;
+
+__global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
     const float* __restrict__ y, const float* __restrict__ rowstat, const float* __restrict__ bstat,
     const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
     float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
@@ -1019,9 +1023,9 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   int kl_blocks = 0;
   if (a->kl) {
     kl = *a->kl;
-    kl_blocks = (int)std::min<int64_t>(cdiv(kl.B * kl.d, 1024), 256);
+    kl_blocks = (int)std::min<int64_t>(cdiv(kl.B * kl.d, kCoefThreads), 256);
   }
-  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B + kl_blocks), dim3(1024), 0, st, a->y, a->rowstat,
+  MPV_LAUNCH("bwd_coef", bwd_coef_kernel, dim3(B + kl_blocks), dim3(kCoefThreads), 0, st, a->y, a->rowstat,
              a->bstat, a->gscal, a->g_indiv, a->g_indiv_label, coef,
              want_planes ? gbound : nullptr, S, B, L, (float)shape->S_total, a->nll_coeff,
              a->c_coeff, a->live, kl, kl_blocks);

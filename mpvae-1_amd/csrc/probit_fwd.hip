@@ -50,7 +50,9 @@ struct FwdParams {
 #endif
 // Tuning constants of the product kernels (each measured; DESIGN.md section 3
 // lists the variants that lost and were removed):
-constexpr int kCombineThreads = 1024;  // fwd_combine: one block per batch row
+// fwd_combine: one block per batch row (512 / 256 threads: C4 0.076 -> 0.115 /
+// 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3)
+constexpr int kCombineThreads = 1024;
 constexpr int kCombineFoldSlabs = 64;  // s-chunk partials fwd_combine sums itself, at most
 constexpr int kFwdWant = 2048;         // target workgroup count of the forward grid (s-chunking)
 constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
@@ -1186,7 +1188,7 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
 }
 
 // One block per batch row b.  rowpart -> rowstat, bstat.
-__global__ __launch_bounds__(1024) void fwd_combine_kernel(const float* __restrict__ y,
+__global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const float* __restrict__ y,
                                                          const float* __restrict__ rowpart,
                                                          float* __restrict__ rowstat,
                                                          float* __restrict__ bstat, int S, int B,
