@@ -877,11 +877,8 @@ constexpr int kDr16TileSmall = 128;
 // noise-plane bytes of the 128 tile at L = z = 38
 constexpr int kDr16TileTiny = 64;
 
-#ifndef MPV_DR_TINY_CPC
-#define MPV_DR_TINY_CPC 2
-#endif
 constexpr int kDrSmallChunksPerCu = 2;  // K chunks per CU for the 128 tile
-constexpr int kDrTinyChunksPerCu = MPV_DR_TINY_CPC;  // and for the 64 tile
+constexpr int kDrTinyChunksPerCu = 2;   // and for the 64 tile (4 and 8 measure the same at C2)
 constexpr int64_t kDrMaxChunkRows = 131072;  // longest split-K chunk (sample rows)
 
 static int dr16_tile(int64_t L, int64_t z) {
