@@ -99,3 +99,35 @@ def test_batched_step_syncs_match_the_reference_semantics():
     got = ms.step_scalars(**vals)
     assert got == {"total_loss": 1.5, "nll_loss": 0.25, "macro_f1": 0.75, "success_updates": 3}
     assert all(type(got[k]) is float for k in ("total_loss", "nll_loss", "macro_f1"))
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1e2])
+def test_train_step_clip_matches_torch(scale):
+    """TrainStep._clip (coefficient cast per gradient dtype, multi-tensor fast
+    path) against torch.nn.utils.clip_grad_norm_(params, 10) on the same
+    gradients, fp32 and fp64 (r_sqrt_sigma) mixed: equal when the norm is
+    under 10, within one fp32 ulp when it clips."""
+    import types
+
+    import mpvae_step
+    args = argparse.Namespace(feature_dim=20, latent_dim=8, label_dim=6, z_dim=4, keep_prob=0.5,
+                              scale_coeff=1.0, residue_sigma="", n_train_sample=4,
+                              n_test_sample=4, mode="train", nll_coeff=0.5, c_coeff=10.0)
+    torch.manual_seed(0)
+    np.random.seed(0)
+    m1 = mpvae.VAE(args)
+    m2 = mpvae.VAE(args)
+    m2.load_state_dict(m1.state_dict())
+    g = torch.Generator().manual_seed(1)
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        gr = torch.randn(p1.shape, generator=g, dtype=torch.float64).to(p1.dtype) * scale
+        p1.grad, p2.grad = gr.clone(), gr.clone()
+    fake_opt = types.SimpleNamespace(defaults={"fused": True}, param_groups=[])
+    ts = mpvae_step.TrainStep(m1, fake_opt, args)
+    ts._clip()
+    torch.nn.utils.clip_grad_norm_(m2.parameters(), 10.0)
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        if scale < 1:
+            assert torch.equal(p1.grad, p2.grad), k
+        else:
+            torch.testing.assert_close(p1.grad, p2.grad, rtol=2 ** -23, atol=0, msg=k)
