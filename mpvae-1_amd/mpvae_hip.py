@@ -196,7 +196,12 @@ def stream_of(device):
     torch.cuda.Stream object costs ~6 (several per compute_loss call)."""
     d = device if isinstance(device, torch.device) else torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
+    if _raw_stream is None:  # a torch without the private query: the public object
+        return ctypes.c_void_p(torch.cuda.current_stream(idx).cuda_stream)
+    return ctypes.c_void_p(_raw_stream(idx))
+
+
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def require_gpu(*tensors):
