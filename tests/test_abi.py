@@ -86,3 +86,27 @@ def test_product_refuses_cpu_tensors():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(H.MPVError, match="not found"):
         H.load_library(str(tmp_path / "nope.so"))
+
+
+def test_linear_host_checks():
+    """mpv_linear's workspace sizing and argument checks run on the host and
+    reject bad problems before any launch (csrc/linear.hip)."""
+    lib = H.load_library()
+    assert lib.mpv_linear_workspace_bytes(0, 4, 4) == 0
+    assert lib.mpv_linear_workspace_bytes(128, 256, 1000) > 0  # split-K partials
+    fake = ctypes.c_void_p(0x1000)  # never dereferenced: every call below fails its checks
+    ok = H.LinearArgs(M=4, N=4, R=4, a=fake, a_si=4, a_sr=1, b=fake, b_sj=4, b_sr=1, ones_col=-1,
+                      alpha=1.0, out=fake, out_si=4)
+    arr = (H.LinearArgs * 3)(ok, ok, ok)
+    assert lib.mpv_linear_batch(arr, 3, None, 0, None) == 1  # at most 2 problems per launch
+    assert b"problems per launch" in lib.mpv_last_error()
+    assert lib.mpv_linear_batch(arr, 0, None, 0, None) == 1
+    no_out = H.LinearArgs(M=4, N=4, R=4, a=fake, b=fake, ones_col=-1, alpha=1.0)
+    assert lib.mpv_linear(ctypes.byref(no_out), None, 0, None) == 1
+    bad_ones = H.LinearArgs(M=4, N=4, R=4, a=fake, a_si=4, a_sr=1, b=fake, b_sj=4, b_sr=1,
+                            ones_col=1, alpha=1.0, out=fake, out_si=4)
+    assert lib.mpv_linear(ctypes.byref(bad_ones), None, 0, None) == 1
+    big = H.LinearArgs(M=128, N=256, R=1000, a=fake, a_si=1000, a_sr=1, b=fake, b_sj=1000,
+                       b_sr=1, ones_col=-1, alpha=1.0, out=fake, out_si=256)
+    assert lib.mpv_linear(ctypes.byref(big), None, 0, None) == 1  # no workspace for the partials
+    assert b"workspace" in lib.mpv_last_error()
