@@ -32,10 +32,11 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 6  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+#define MPV_ABI_VERSION 7  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
                               5: T rows padded to roundup(L, 4) floats;
                               6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
-                                 dR64 and kl */
+                                 dR64 and kl;
+                              7: mpv_linear_batch takes up to 4 problems */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -303,8 +304,9 @@ typedef struct mpv_linear_args {
 size_t mpv_linear_workspace_bytes(int64_t M, int64_t N, int64_t R);
 int mpv_linear(const mpv_linear_args* args, void* workspace, size_t workspace_bytes, void* stream);
 
-/* n (1..2) independent mpv_linear problems in one launch pair (a layer's dx
- * and dW + db); the workspace is the sum of the problems' own, in order. */
+/* n (1..4) independent mpv_linear problems in one launch pair (a layer's dx
+ * and dW + db; two heads and their gradients); the workspace is the sum of
+ * the problems' own, in order. */
 size_t mpv_linear_batch_workspace_bytes(const mpv_linear_args* args, int n);
 int mpv_linear_batch(const mpv_linear_args* args, int n, void* workspace, size_t workspace_bytes,
                      void* stream);

@@ -19,7 +19,8 @@
 // reduction rows per LDS stage (64 measured no faster: 0.46 vs 0.36 ms for
 // the 43 GEMMs of a C3 training step); the next stage's global loads are
 // issued before the current stage's MFMAs (register double buffer).
-// Independent GEMMs (a layer's dx and dW) go in one launch: up to
+// Independent GEMMs (a layer's dx and dW; both heads of an encoder, or of
+// the stacked decoder, with their gradients) go in one launch: up to
 // kLinMaxProb problems, told apart by blockIdx.z ranges.
 #include "abi_util.h"
 #include "mpv_common.h"
@@ -112,7 +113,7 @@ MPV_DEV void lin_finish(const LinParams& p, int64_t i, int64_t j, float s) {
   p.out[i * p.out_si + j] = s;
 }
 
-constexpr int kLinMaxProb = 2;
+constexpr int kLinMaxProb = 4;
 
 struct LinBatch {
   LinParams p[kLinMaxProb];
@@ -125,11 +126,14 @@ struct LinBatch {
 __global__ __launch_bounds__(kLinThreads) void lin_gemm_kernel(LinBatch bt) {
   __shared__ float sa[kLinStep][kLinTile + 4];
   __shared__ float sb[kLinStep][kLinTile + 4];
-  const int q = (bt.n > 1 && (int)blockIdx.z >= bt.zoff[1]) ? 1 : 0;
-  const LinParams p = q ? bt.p[1] : bt.p[0];
-  if ((int)blockIdx.x >= (q ? bt.ti[1] : bt.ti[0]) || (int)blockIdx.y >= (q ? bt.tj[1] : bt.tj[0]))
+  int q = 0;  // the problem whose chunk range holds blockIdx.z
+#pragma unroll
+  for (int k = 1; k < kLinMaxProb; ++k)
+    if (k < bt.n && (int)blockIdx.z >= bt.zoff[k]) q = k;
+  const LinParams& p = bt.p[q];
+  if ((int)blockIdx.x >= bt.ti[q] || (int)blockIdx.y >= bt.tj[q])
     return;  // this problem has fewer tiles than the grid
-  const int split = (int)blockIdx.z - (q ? bt.zoff[1] : 0);
+  const int split = (int)blockIdx.z - bt.zoff[q];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i0 = (int64_t)blockIdx.x * kLinTile, j0 = (int64_t)blockIdx.y * kLinTile;
   const int64_t rb = (int64_t)split * p.chunk, re = min(p.R, rb + p.chunk);
@@ -190,7 +194,10 @@ __global__ __launch_bounds__(kLinThreads) void lin_gemm_kernel(LinBatch bt) {
 __global__ __launch_bounds__(256) void lin_reduce_kernel(LinBatch bt) {
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < bt.eoff[bt.n];
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (bt.n > 1 && e >= bt.eoff[1]) ? 1 : 0;
+    int q = 0;
+#pragma unroll
+    for (int k = 1; k < kLinMaxProb; ++k)
+      if (k < bt.n && e >= bt.eoff[k]) q = k;
     const LinParams& p = bt.p[q];
     const int64_t le = e - bt.eoff[q], n = p.M * p.N;
     const int nsplit = bt.zoff[q + 1] - bt.zoff[q];

@@ -108,6 +108,8 @@ class VAE(nn.Module):
         return x
 
     def _heads(self, h, mu, logvar):
+        if self.linear_backend == "hip":  # both heads in one launch
+            return mpvae_linear.heads(h, mu, logvar, self.scale_coeff)
         return (self._lin(mu, h, alpha=self.scale_coeff),
                 self._lin(logvar, h, alpha=self.scale_coeff))
 
@@ -151,14 +153,24 @@ class VAE(nn.Module):
 
         Both encoders are evaluated first and reparameterised by ONE fused
         launch.  RNG draws keep the reference order: label-encoder dropouts,
-        label eps, feature-encoder dropouts, feature eps (mpvae.py:86-100)."""
+        label eps, feature-encoder dropouts, feature eps (mpvae.py:86-100).
+        On mpv_linear the two decoders, which share fd_x1 / fd_x2, run as one
+        pass over both inputs stacked (no dropout there: same values)."""
         mu_e, lv_e = self.label_encode(torch.cat((feature, label), 1))
         eps_e = self.reparam_noise(lv_e)
         mu_x, lv_x = self.feat_encode(feature)
         eps_x = self.reparam_noise(lv_x)
         z_e, z_x = FusedReparam.apply(mu_e, lv_e, eps_e, mu_x, lv_x, eps_x)
-        label_out = self.label_decode(torch.cat((feature, z_e), 1))
-        feat_out = self.feat_decode(torch.cat((feature, z_x), 1))
+        if self.linear_backend == "hip":
+            # both decoders share fd_x1 / fd_x2 (mpvae.py:31-32): run them
+            # once on the two inputs stacked, then the two heads on their rows
+            B = feature.shape[0]
+            zz = torch.cat((torch.cat((feature, feature), 0), torch.cat((z_e, z_x), 0)), 1)
+            h = self._lin(self.fd_x2, self._lin(self.fd_x1, zz, relu=True), relu=True)
+            label_out, feat_out = mpvae_linear.row_heads(h, self.label_mp_mu, self.feat_mp_mu, B)
+        else:
+            label_out = self.label_decode(torch.cat((feature, z_e), 1))
+            feat_out = self.feat_decode(torch.cat((feature, z_x), 1))
         return label_out, mu_e, lv_e, feat_out, mu_x, lv_x
 
 

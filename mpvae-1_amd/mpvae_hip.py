@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 

@@ -30,7 +30,7 @@ def _problem(M, N, R, a, a_si, a_sr, b, b_sj, b_sr, out, out_si, *, a_mask=None,
 
 
 def _launch(device, *problems):
-    """One launch (pair) for 1-2 independent problems."""
+    """One launch (pair) for 1-4 independent problems."""
     lib = H.load_library()
     arr = (H.LinearArgs * len(problems))(*problems)
     nbytes = lib.mpv_linear_batch_workspace_bytes(arr, len(problems))
@@ -96,6 +96,136 @@ class HipLinear(torch.autograd.Function):
         return gx, gw, gb, None, None
 
 
+def _check_params(x, *wb):
+    H.require_gpu(x, *wb)
+    if x.dtype != torch.float32 or any(t is not None and t.dtype != torch.float32 for t in wb):
+        raise TypeError("mpv_linear computes in fp32 (the reference's nn.Linear dtype)")
+    if x.dim() != 2:
+        raise ValueError(f"mpv_linear takes (batch, features) inputs, got {tuple(x.shape)}")
+    for w, b in zip(wb[::2], wb[1::2]):
+        if w.dim() != 2 or w.shape[1] != x.shape[1] or (b is not None and b.shape != (w.shape[0],)):
+            raise ValueError(f"bad Linear parameters for input {tuple(x.shape)}: weight "
+                             f"{tuple(w.shape)}, bias {None if b is None else tuple(b.shape)}")
+
+
+class HipLinearHeads(torch.autograd.Function):
+    """Two Linear heads of one input, ``(alpha * a(x), alpha * b(x))`` -- an
+    encoder's mu and logvar (reference mpvae.py:54-55,63-64) -- in one launch
+    pair; the backward's dW, db of both heads and both dx terms in one more."""
+
+    @staticmethod
+    def forward(ctx, x, wa, ba, wb, bb, alpha):
+        _check_params(x, wa, ba, wb, bb)
+        x = _rows(x)
+        wa, wb = wa.contiguous(), wb.contiguous()
+        M, K = x.shape
+        ys = []
+        problems = []
+        for w, b in ((wa, ba), (wb, bb)):
+            y = torch.empty((M, w.shape[0]), dtype=torch.float32, device=x.device)
+            problems.append(_problem(M, w.shape[0], K, x, x.stride(0), 1, w, K, 1, y, w.shape[0],
+                                     bias=None if b is None else b.contiguous(), alpha=alpha))
+            ys.append(y)
+        _launch(x.device, *problems)
+        ctx.save_for_backward(x, wa, wb)
+        ctx.alpha, ctx.has_bias = alpha, (ba is not None, bb is not None)
+        return ys[0], ys[1]
+
+    @staticmethod
+    def backward(ctx, ga, gb_):
+        x, wa, wb = ctx.saved_tensors
+        M, K = x.shape
+        dev = x.device
+        need = ctx.needs_input_grad
+        grads = [None] * 6
+        problems, dxs = [], []
+        for k, (w, g) in enumerate(((wa, ga), (wb, gb_))):
+            g = g.contiguous()
+            N = w.shape[0]
+            if need[0]:
+                dx = torch.empty((M, K), dtype=torch.float32, device=dev)
+                problems.append(_problem(M, K, N, g, N, 1, w, 1, K, dx, K, a_scale=ctx.alpha))
+                dxs.append(dx)
+            if need[1 + 2 * k] or need[2 + 2 * k]:
+                hb = ctx.has_bias[k]
+                gw = torch.empty((N, K), dtype=torch.float32, device=dev)
+                gbias = torch.empty((N,), dtype=torch.float32, device=dev) if hb else None
+                problems.append(_problem(N, K + (1 if hb else 0), M, g, 1, N, x, 1, x.stride(0),
+                                         gw, K, a_scale=ctx.alpha, ones_col=K if hb else -1,
+                                         out_col=gbias))
+                grads[1 + 2 * k], grads[2 + 2 * k] = gw, gbias
+        if problems:
+            _launch(dev, *problems)
+        if need[0]:
+            grads[0] = dxs[0].add_(dxs[1])
+        return tuple(grads)
+
+
+class HipRowHeads(torch.autograd.Function):
+    """Two Linear heads on the two row blocks of one stacked input,
+    ``(a(h[:n_a]), b(h[n_a:]))`` -- the label and feature decoders' last
+    layers after their shared fd_x1 / fd_x2 ran on both inputs stacked
+    (reference mpvae.py:76-84) -- in one launch pair, and their backward (the
+    stacked d h and both dW, db) in one more."""
+
+    @staticmethod
+    def forward(ctx, h, wa, ba, wb, bb, n_a):
+        _check_params(h, wa, ba, wb, bb)
+        h = _rows(h)
+        wa, wb = wa.contiguous(), wb.contiguous()
+        M, K = h.shape
+        if not 0 <= n_a <= M:
+            raise ValueError(f"row split {n_a} outside 0..{M}")
+        blocks = ((0, n_a, wa, ba), (n_a, M - n_a, wb, bb))
+        ys, problems = [], []
+        for r0, m, w, b in blocks:
+            y = torch.empty((m, w.shape[0]), dtype=torch.float32, device=h.device)
+            problems.append(_problem(m, w.shape[0], K, h[r0:], h.stride(0), 1, w, K, 1, y,
+                                     w.shape[0], bias=None if b is None else b.contiguous()))
+            ys.append(y)
+        _launch(h.device, *problems)
+        ctx.save_for_backward(h, wa, wb)
+        ctx.n_a, ctx.has_bias = n_a, (ba is not None, bb is not None)
+        return ys[0], ys[1]
+
+    @staticmethod
+    def backward(ctx, ga, gb_):
+        h, wa, wb = ctx.saved_tensors
+        M, K = h.shape
+        dev = h.device
+        need = ctx.needs_input_grad
+        grads = [None] * 6
+        gh = torch.empty((M, K), dtype=torch.float32, device=dev) if need[0] else None
+        problems = []
+        for k, (r0, m, w, g) in enumerate(((0, ctx.n_a, wa, ga), (ctx.n_a, M - ctx.n_a, wb, gb_))):
+            g = g.contiguous()
+            N = w.shape[0]
+            if need[0]:
+                problems.append(_problem(m, K, N, g, N, 1, w, 1, K, gh[r0:], K))
+            if need[1 + 2 * k] or need[2 + 2 * k]:
+                hb = ctx.has_bias[k]
+                gw = torch.empty((N, K), dtype=torch.float32, device=dev)
+                gbias = torch.empty((N,), dtype=torch.float32, device=dev) if hb else None
+                problems.append(_problem(N, K + (1 if hb else 0), m, g, 1, N, h[r0:], 1,
+                                         h.stride(0), gw, K, ones_col=K if hb else -1,
+                                         out_col=gbias))
+                grads[1 + 2 * k], grads[2 + 2 * k] = gw, gbias
+        if problems:
+            _launch(dev, *problems)
+        grads[0] = gh
+        return tuple(grads)
+
+
 def linear(x, layer, relu=False, alpha=1.0):
     """act(alpha * layer(x)) on the matrix cores, act = ReLU if `relu`."""
     return HipLinear.apply(x, layer.weight, layer.bias, bool(relu), float(alpha))
+
+
+def heads(x, a, b, alpha=1.0):
+    """(alpha * a(x), alpha * b(x)) for two Linear layers of one input."""
+    return HipLinearHeads.apply(x, a.weight, a.bias, b.weight, b.bias, float(alpha))
+
+
+def row_heads(h, a, b, n_a):
+    """(a(h[:n_a]), b(h[n_a:])) for two Linear layers on the row blocks of h."""
+    return HipRowHeads.apply(h, a.weight, a.bias, b.weight, b.bias, int(n_a))

@@ -97,8 +97,8 @@ def test_linear_host_checks():
     fake = ctypes.c_void_p(0x1000)  # never dereferenced: every call below fails its checks
     ok = H.LinearArgs(M=4, N=4, R=4, a=fake, a_si=4, a_sr=1, b=fake, b_sj=4, b_sr=1, ones_col=-1,
                       alpha=1.0, out=fake, out_si=4)
-    arr = (H.LinearArgs * 3)(ok, ok, ok)
-    assert lib.mpv_linear_batch(arr, 3, None, 0, None) == 1  # at most 2 problems per launch
+    arr = (H.LinearArgs * 5)(ok, ok, ok, ok, ok)
+    assert lib.mpv_linear_batch(arr, 5, None, 0, None) == 1  # at most 4 problems per launch
     assert b"problems per launch" in lib.mpv_last_error()
     assert lib.mpv_linear_batch(arr, 0, None, 0, None) == 1
     no_out = H.LinearArgs(M=4, N=4, R=4, a=fake, b=fake, ones_col=-1, alpha=1.0)

@@ -163,7 +163,9 @@ def test_vae_linear_backends_agree():
                     masks.append((y > 0).float())
                 return y
         else:
-            forced = iter(list(masks))
+            # hip ran the two decoders stacked (rows :B label, B: feature)
+            enc, (d1, d2) = masks[:5], masks[5:]
+            forced = iter(enc + [d1[:128], d2[:128], d1[128:], d2[128:]])
 
             def lin(layer, x, relu=False, alpha=1.0):
                 y = layer(x) * alpha
@@ -179,7 +181,7 @@ def test_vae_linear_backends_agree():
         res[backend] = ([o.detach() for o in out],
                         {k: p.grad.clone() for k, p in model.named_parameters()
                          if p.grad is not None})
-    assert len(masks) == 9  # encoders 2 + 3 ReLU layers, two decoder passes of 2
+    assert len(masks) == 7  # encoders 2 + 3 ReLU layers, the stacked decoder pass of 2
     errs = {}
     for i, (a, b) in enumerate(zip(res["hip"][0], res["torch"][0])):
         errs[f"out{i}"] = rel_err(a.cpu(), b.cpu())
@@ -188,3 +190,56 @@ def test_vae_linear_backends_agree():
     record("vae_linear_hip_vs_torch", errs)
     for k, e in errs.items():
         assert e < LINEAR_VAE_RTOL, (k, e)
+
+
+@pytest.mark.parametrize("M,K,Na,Nb,alpha", [(128, 256, 50, 50, 1.3), (7, 20, 6, 3, 1.0),
+                                             (512, 256, 50, 50, 0.7)])
+def test_heads_match_fp64(M, K, Na, Nb, alpha):
+    """mpvae_linear.heads (an encoder's mu and logvar heads in one launch)
+    against fp64: outputs, d x (both heads' terms summed), dW and db of each."""
+    torch.manual_seed(M + K)
+    la, lb = torch.nn.Linear(K, Na).to(DEV), torch.nn.Linear(K, Nb).to(DEV)
+    x = torch.randn((M, K), device=DEV, requires_grad=True)
+    ya, yb = mpvae_linear.heads(x, la, lb, alpha)
+    ga, gb = torch.randn_like(ya), torch.randn_like(yb)
+    torch.autograd.backward((ya, yb), (ga, gb))
+    with torch.no_grad():
+        xd = x.detach().double()
+        refs = [alpha * (xd @ l.weight.double().T + l.bias.double()) for l in (la, lb)]
+        gx = alpha * (ga.double() @ la.weight.double() + gb.double() @ lb.weight.double())
+    errs = {"ya": rel_err(ya.detach().cpu(), refs[0].cpu()),
+            "yb": rel_err(yb.detach().cpu(), refs[1].cpu()),
+            "dx": rel_err(x.grad.cpu(), gx.cpu())}
+    for n, l, g in (("a", la, ga), ("b", lb, gb)):
+        errs["dW" + n] = rel_err(l.weight.grad.cpu(), (alpha * g.double().T @ xd).cpu())
+        errs["db" + n] = rel_err(l.bias.grad.cpu(), (alpha * g.double().sum(0)).cpu())
+    record(f"linear_heads_{M}_{K}_{Na}_{Nb}", errs)
+    for k, e in errs.items():
+        assert e < LINEAR_RTOL, (k, e)
+
+
+@pytest.mark.parametrize("M,n_a,K,Na,Nb", [(256, 128, 512, 38, 38), (7, 3, 20, 5, 4),
+                                           (64, 0, 33, 6, 6), (64, 64, 33, 6, 6)])
+def test_row_heads_match_fp64(M, n_a, K, Na, Nb):
+    """mpvae_linear.row_heads (the stacked decoders' two last layers, one per
+    row block) against fp64, empty blocks included."""
+    torch.manual_seed(M + n_a + K)
+    la, lb = torch.nn.Linear(K, Na).to(DEV), torch.nn.Linear(K, Nb).to(DEV)
+    h = torch.randn((M, K), device=DEV, requires_grad=True)
+    ya, yb = mpvae_linear.row_heads(h, la, lb, n_a)
+    assert ya.shape == (n_a, Na) and yb.shape == (M - n_a, Nb)
+    ga, gb = torch.randn_like(ya), torch.randn_like(yb)
+    torch.autograd.backward((ya, yb), (ga, gb))
+    with torch.no_grad():
+        hd = h.detach().double()
+        ra = hd[:n_a] @ la.weight.double().T + la.bias.double()
+        rb = hd[n_a:] @ lb.weight.double().T + lb.bias.double()
+        gh = torch.cat((ga.double() @ la.weight.double(), gb.double() @ lb.weight.double()), 0)
+    errs = {"ya": rel_err(ya.detach().cpu(), ra.cpu()), "yb": rel_err(yb.detach().cpu(), rb.cpu()),
+            "dh": rel_err(h.grad.cpu(), gh.cpu())}
+    for n, l, g, rows in (("a", la, ga, hd[:n_a]), ("b", lb, gb, hd[n_a:])):
+        errs["dW" + n] = rel_err(l.weight.grad.cpu(), (g.double().T @ rows).cpu())
+        errs["db" + n] = rel_err(l.bias.grad.cpu(), g.double().sum(0).cpu())
+    record(f"linear_row_heads_{M}_{n_a}_{K}", errs)
+    for k, e in errs.items():
+        assert e < LINEAR_RTOL, (k, e)
