@@ -539,4 +539,18 @@ MPV_DEV void box_muller(uint32_t we, uint32_t wo, float& n0, float& n1) {
   n1 = r * __builtin_amdgcn_sinf(v);
 }
 
+// Compute units of the current device (host side; 256 when it cannot be
+// queried, e.g. in a build container without a GPU).
+inline int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 }  // namespace mpv

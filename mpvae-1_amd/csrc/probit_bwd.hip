@@ -886,18 +886,6 @@ static int dr16_tile(int64_t L, int64_t z) {
   return (L <= kDr16TileSmall && z <= kDr16TileSmall) ? kDr16TileSmall : kDr16Tile;
 }
 
-static int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-  }
-  return n;
-}
-
 static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   BwdPlan pl;
   const int64_t L = s->L, S = s->S_local, B = s->B, z = s->z;

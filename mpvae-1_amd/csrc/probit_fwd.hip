@@ -54,7 +54,7 @@ struct FwdParams {
 // 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3)
 constexpr int kCombineThreads = 1024;
 constexpr int kCombineFoldSlabs = 64;  // s-chunk partials fwd_combine sums itself, at most
-constexpr int kFwdWant = 2048;         // target workgroup count of the forward grid (s-chunking)
+constexpr int kFwdWant = 2048;         // fp32 mode: target workgroup count of the forward grid
 constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
@@ -1324,8 +1324,12 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
-  // enough workgroups to fill 256 CUs several times; fewer s-chunks = fewer partials
-  int64_t want = cdiv(kFwdWant, s->B * (int64_t)pl.nNt);
+  // 3xf16: s-chunks until the grid is one round of resident workgroups (2
+  // per CU for the 48-label tile, 1 for the 8-wave tiles); longer runs per
+  // workgroup amortize its prologue (C3 step 0.534 -> 0.510 ms against a
+  // 2048-workgroup target, C2 the same; C4 has one s-chunk either way)
+  const int64_t target = f16 ? (pl.cfg == 0 ? 2 : 1) * (int64_t)num_cus() : kFwdWant;
+  int64_t want = cdiv(target, s->B * (int64_t)pl.nNt);
   if (want < 1) want = 1;
   if (want > pl.nSt) want = pl.nSt;
   pl.tps = (int)cdiv(pl.nSt, want);
