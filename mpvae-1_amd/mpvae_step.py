@@ -16,6 +16,8 @@ fairsoft_train.py:154-162).  Each sync drains the stream.  Here:
 Both are torch glue around the loop, not kernels of the hot path: they run on
 whatever device the tensors live on.
 """
+import functools
+
 import torch
 
 
@@ -98,8 +100,14 @@ class TrainStep:
                 by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
         if not by_dtype:
             return
-        norms = [n for grads in by_dtype.values() for n in torch._foreach_norm(grads, 2.0)]
-        total = torch.linalg.vector_norm(torch.stack(norms), 2.0)
+        # torch stacks the per-tensor norms of every dtype into one promoted
+        # (fp64) vector, which casts each fp32 norm in a launch of its own (26
+        # at the VAE); here each dtype's norms are stacked and cast once: the
+        # same vector, in the same order
+        wide = functools.reduce(torch.promote_types, by_dtype)
+        parts = [torch.stack(torch._foreach_norm(grads, 2.0)).to(wide)
+                 for grads in by_dtype.values()]
+        total = torch.linalg.vector_norm(parts[0] if len(parts) == 1 else torch.cat(parts), 2.0)
         coef = torch.clamp(self.max_grad_norm / (total + 1e-6), max=1.0)
         for dt, grads in by_dtype.items():
             torch._foreach_mul_(grads, coef.to(dt))
