@@ -228,6 +228,9 @@ RANDOM_CASES = [
     (97, 33, 3, 100, 8),         # first L of the 128-label tile; noise planes 128 wide
     (25, 10, 6, 64, 8),          # fairsoft adult-like dims (SURVEY fixture F3)
     (4096, 4096, 1, 40, 8),      # C5 dims (16 label tiles, 128 K stages), S < one tile
+    # minimal sizes: one sample, one noise dimension, one batch row, d = 1
+    (2, 1, 1, 1, 1),
+    (3, 2, 2, 2, 1),
 ]
 
 
