@@ -32,11 +32,12 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 7  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+#define MPV_ABI_VERSION 8  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
                               5: T rows padded to roundup(L, 4) floats;
                               6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
                                  dR64 and kl;
-                              7: mpv_linear_batch takes up to 4 problems */
+                              7: mpv_linear_batch takes up to 4 problems
+                              8: mpv_adam_step */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -311,12 +312,41 @@ size_t mpv_linear_batch_workspace_bytes(const mpv_linear_args* args, int n);
 int mpv_linear_batch(const mpv_linear_args* args, int n, void* workspace, size_t workspace_bytes,
                      void* stream);
 
+/* ------------------------------------------------------ Adam (TrainStep) */
+/* One Adam update over up to MPV_ADAM_MAX_TENSORS parameter tensors, fp32 and
+ * fp64 mixed, in one launch; replaces optimizer.step() of
+ * torch.optim.Adam(params, lr, betas, eps, weight_decay) (fairsoft_train.py:57,
+ * :146) inside mpvae_step.TrainStep, with torch's fused-Adam arithmetic
+ * (L2 weight decay, no amsgrad / maximize).  `step` is the tensor's device
+ * step count, already incremented for this update (torch's capturable
+ * protocol); bias corrections come from it.  found_inf (may be NULL): when
+ * *found_inf == 1 nothing is written. */
+#define MPV_ADAM_MAX_TENSORS 32
+typedef struct mpv_adam_tensor {
+  void* param;
+  const void* grad;
+  void* exp_avg;
+  void* exp_avg_sq;
+  const float* step;
+  int64_t numel;
+  int is_f64;  /* 0: float32 tensors, 1: float64 */
+} mpv_adam_tensor;
+
+typedef struct mpv_adam_args {
+  int n;
+  mpv_adam_tensor t[MPV_ADAM_MAX_TENSORS];
+  double lr, beta1, beta2, weight_decay, eps;
+  const float* found_inf;
+} mpv_adam_args;
+
+int mpv_adam_step(const mpv_adam_args* args, void* stream);
+
 /* ------------------------------------------------------------ measurement */
 /* When enabled, every kernel launch of the library is bracketed by a pair of
  * HIP events on the launch stream (bench.py's per-kernel roofline timing).
  * Kernel names: noise_philox, probit_fwd, fwd_combine, finalize, bwd_coef,
  * bwd_elem, dR_gemm, sum_slabs, convert, bstat_combine, reparam_fwd,
- * reparam_bwd, kl_bwd, linear.  Query synchronises the recorded events. */
+ * reparam_bwd, kl_bwd, linear, adam.  Query synchronises the recorded events. */
 int mpv_timing_enable(int on);
 int mpv_timing_reset(void);
 int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms);

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -101,6 +101,22 @@ class LinearArgs(ctypes.Structure):
                 ("out_si", ctypes.c_int64), ("out_col", vp)]
 
 
+ADAM_MAX_TENSORS = 32
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", vp), ("grad", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("step", vp),
+                ("numel", ctypes.c_int64), ("is_f64", ctypes.c_int)]
+
+
+class AdamArgs(ctypes.Structure):
+    """mpv_adam_args: one Adam update over up to 32 tensors (adam.hip)."""
+    _fields_ = [("n", ctypes.c_int), ("t", AdamTensor * ADAM_MAX_TENSORS),
+                ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("weight_decay", ctypes.c_double), ("eps", ctypes.c_double),
+                ("found_inf", vp)]
+
+
 class FairArgs(ctypes.Structure):
     _fields_ = [("label_z", vp), ("feat_z", vp), ("w", vp), ("order", vp), ("goff", vp),
                 ("gid", vp), ("B", ctypes.c_int64), ("L", ctypes.c_int64), ("T", ctypes.c_int64),
@@ -140,6 +156,7 @@ SIGNATURES = {
     "mpv_linear_batch_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(LinearArgs), ctypes.c_int]),
     "mpv_linear_batch": (ctypes.c_int, [ctypes.POINTER(LinearArgs), ctypes.c_int, vp,
                                         ctypes.c_size_t, vp]),
+    "mpv_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamArgs), vp]),
     "mpv_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "mpv_timing_reset": (ctypes.c_int, []),
     "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
@@ -215,7 +232,7 @@ def require_gpu(*tensors):
 
 KERNELS = ["noise_philox", "split", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
            "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
-           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics", "linear"]
+           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics", "linear", "adam"]
 
 
 def kernel_times():

@@ -16,6 +16,7 @@ fairsoft_train.py:154-162).  Each sync drains the stream.  Here:
 Both are torch glue around the loop, not kernels of the hot path: they run on
 whatever device the tensors live on.
 """
+import ctypes
 import functools
 
 import torch
@@ -52,6 +53,68 @@ def step_scalars(**tensors):
     return out
 
 
+def _native_adam(opt):
+    """True when ``opt`` is a plain fused torch.optim.Adam that mpv_adam_step
+    reproduces (L2 weight decay, float lr, no amsgrad / maximize /
+    decoupled weight decay, CUDA parameters)."""
+    if type(opt) is not torch.optim.Adam:
+        return False
+    for g in opt.param_groups:
+        if (not g.get("fused") or g.get("amsgrad") or g.get("maximize")
+                or g.get("differentiable") or g.get("decoupled_weight_decay", False)
+                or isinstance(g["lr"], torch.Tensor) or isinstance(g["betas"][0], torch.Tensor)):
+            return False
+        if any(p.device.type != "cuda" or p.dtype not in (torch.float32, torch.float64)
+               for p in g["params"]):
+            return False
+    return True
+
+
+def adam_step(opt, found_inf):
+    """optimizer.step() of a fused torch.optim.Adam in one mpv_adam_step launch
+    per parameter group (csrc/adam.hip) instead of torch's multi-tensor kernel,
+    which runs the VAE's 1.5 M parameters on ~25 workgroups (DESIGN.md
+    section 11).  Same state (``step``, ``exp_avg``, ``exp_avg_sq`` in
+    ``opt.state``), same step-count protocol as torch's capturable fused path
+    (+1 before, -found_inf after), same per-element arithmetic; nothing is
+    written when ``found_inf`` is 1."""
+    import mpvae_hip as H
+    lib = H.load_library()
+    for g in opt.param_groups:
+        params = [p for p in g["params"] if p.grad is not None]
+        if not params:
+            continue
+        for p in params:
+            st = opt.state[p]
+            if len(st) == 0:  # torch's _init_group for fused Adam
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        steps = [opt.state[p]["step"] for p in params]
+        torch._foreach_add_(steps, 1)
+        beta1, beta2 = g["betas"]
+        for c in range(0, len(params), H.ADAM_MAX_TENSORS):
+            a = H.AdamArgs(n=0, lr=float(g["lr"]), beta1=float(beta1), beta2=float(beta2),
+                           weight_decay=float(g["weight_decay"]), eps=float(g["eps"]),
+                           found_inf=H.ptr(found_inf))
+            for p in params[c:c + H.ADAM_MAX_TENSORS]:
+                st = opt.state[p]
+                ts = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
+                if not all(t.is_contiguous() and t.dtype == p.dtype for t in ts):
+                    raise ValueError("mpv_adam_step needs contiguous parameters, gradients "
+                                     "and state of the parameter's dtype")
+                a.t[a.n] = H.AdamTensor(param=p.data_ptr(), grad=p.grad.data_ptr(),
+                                        exp_avg=st["exp_avg"].data_ptr(),
+                                        exp_avg_sq=st["exp_avg_sq"].data_ptr(),
+                                        step=st["step"].data_ptr(), numel=p.numel(),
+                                        is_f64=int(p.dtype == torch.float64))
+                a.n += 1
+            H.check(lib.mpv_adam_step(ctypes.byref(a), H.stream_of(params[0].device)),
+                    "mpv_adam_step")
+        if found_inf is not None:
+            torch._foreach_sub_(steps, [found_inf] * len(steps))
+
+
 class TrainStep:
     """The loop body of fairsoft_train.py:47-146 (penalty-free) as one call:
     ``model(label, feat)`` -> ``compute_loss`` -> ``backward`` ->
@@ -69,13 +132,16 @@ class TrainStep:
     A scheduler stepped only on applied updates (fairsoft_train.py:143-144)
     needs the host, and stays the caller's (eager) business."""
 
-    def __init__(self, model, optimizer, args, max_grad_norm=10.0, advance_seed=True):
+    def __init__(self, model, optimizer, args, max_grad_norm=10.0, advance_seed=True,
+                 native_adam=True):
         if not optimizer.defaults.get("fused"):
             raise ValueError("TrainStep gates the update on the device: use a fused optimizer "
                              "(torch.optim.Adam(..., fused=True))")
         self.model, self.opt, self.args = model, optimizer, args
         self.max_grad_norm = max_grad_norm
         self.advance_seed = advance_seed
+        # a plain fused Adam steps in mpv_adam_step (adam_step); others in torch
+        self.native_adam = bool(native_adam) and _native_adam(optimizer)
         self.params = [p for p in model.parameters() if p.requires_grad]
         dev = self.params[0].device
         self.updates = torch.zeros((), dtype=torch.int64, device=dev)
@@ -132,11 +198,14 @@ class TrainStep:
                 by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
         for grads in by_dtype.values():
             torch._amp_foreach_non_finite_check_and_unscale_(grads, self.found_inf, self._one)
-        self.opt.found_inf = self.found_inf
-        try:
-            self.opt.step()
-        finally:
-            del self.opt.found_inf
+        if self.native_adam:
+            adam_step(self.opt, self.found_inf)
+        else:
+            self.opt.found_inf = self.found_inf
+            try:
+                self.opt.step()
+            finally:
+                del self.opt.found_inf
         self.updates.add_(1 - self.found_inf.to(torch.int64))
         return res
 

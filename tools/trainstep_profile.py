@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--linear", default="hip", choices=["hip", "torch"])
     # also list the aten ops of one eager TrainStep call (what issues the launches)
     ap.add_argument("--ops", action="store_true")
+    # TrainStep's Adam: mpv_adam_step (default) or torch's fused kernel, for A/B
+    ap.add_argument("--torch-adam", action="store_true")
     cli = ap.parse_args()
     dev = torch.device("cuda", 0)
     if cli.blas:
@@ -113,7 +115,7 @@ def main():
     phases = {n: round(v / cli.steps, 4) for n, v in zip(names, acc)}
 
     args, model, opt, label, feat = build(cli.config, dev, fused=True, linear=cli.linear)
-    ts = mpvae_step.TrainStep(model, opt, args)
+    ts = mpvae_step.TrainStep(model, opt, args, native_adam=not cli.torch_adam)
     for _ in range(3):
         ts(label, feat)
     ts_ms = timed(lambda: ts(label, feat), cli.steps)
@@ -146,7 +148,7 @@ def main():
     if cli.ops:
         from torch.profiler import ProfilerActivity, profile
         _, model2, opt2, _, _ = build(cli.config, dev, fused=True, linear=cli.linear)
-        ts2 = mpvae_step.TrainStep(model2, opt2, args)
+        ts2 = mpvae_step.TrainStep(model2, opt2, args, native_adam=not cli.torch_adam)
         ts2(label, feat)
         torch.cuda.synchronize()
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
@@ -163,7 +165,8 @@ def main():
                                  "nll_coeff": nllc, "c_coeff": cc, "lr": lr},
                       "steps": cli.steps, "eager_ms": round(eager_ms, 4),
                       "phases_ms": phases, "trainstep_ms": round(ts_ms, 4),
-                      "graph_ms": round(graph_ms, 4), "updates": int(ts.updates),
+                      "graph_ms": round(graph_ms, 4), "adam": "torch" if cli.torch_adam else "mpv_adam_step",
+                      "updates": int(ts.updates),
                       "loss_finite": bool(torch.isfinite(ts.out[0]).item()),
                       "kernels": kernels}), flush=True)
 
