@@ -46,6 +46,10 @@ from mpvae_ops import ElboConfig, FusedReparam, ProbitELBO, SingleReparam
 
 __all__ = ["VAE", "compute_loss"]
 
+# the encoders' dropout backward folded into mpv_linear (same values; False:
+# nn.Dropout's own backward kernel, for A/B)
+FOLD_DROPOUT = True
+
 # (attribute, in_features, out_features) in the reference's construction order
 # (mpvae.py:14-32).  The order fixes the torch init draws and the state_dict
 # key order, so seeded runs and existing .pkl checkpoints carry over.
@@ -103,8 +107,15 @@ class VAE(nn.Module):
 
     # -- encoders (mpvae.py:51-64)
     def _mlp(self, x, layers):
+        drop = self.dropout
+        fold = (FOLD_DROPOUT and self.linear_backend == "hip" and type(drop) is nn.Dropout
+                and drop.training
+                and drop.p > 0.0 and not drop.inplace)
         for lin in layers:
-            x = self.dropout(self._lin(lin, x, relu=True))
+            if fold:  # torch's dropout kernel, its backward folded into mpv_linear
+                x = mpvae_linear.linear(x, lin, True, 1.0, drop.p)
+            else:
+                x = drop(self._lin(lin, x, relu=True))
         return x
 
     def _heads(self, h, mu, logvar):

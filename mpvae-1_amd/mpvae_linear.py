@@ -45,8 +45,18 @@ def _rows(x):
 
 
 class HipLinear(torch.autograd.Function):
+    """act(alpha * (x W^T + b)), then (drop_p > 0) torch's own dropout.
+
+    With dropout the forward output is ``native_dropout(relu(...), p)`` --
+    the kernel nn.Dropout runs, same generator, same masks -- and the
+    backward folds the dropout backward into the gradient GEMMs' operand
+    load: out = y * keep / (1 - p) is > 0 exactly where the ReLU passes (y > 0)
+    AND the element was kept, so masking the upstream gradient by (out > 0)
+    and scaling it by 1 / (1 - p) gives torch's masked_scale + threshold_backward
+    values bit for bit, without their launches (alpha must be 1)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, relu, alpha):
+    def forward(ctx, x, weight, bias, relu, alpha, drop_p=0.0):
         H.require_gpu(x, weight, bias)
         if x.dtype != torch.float32 or weight.dtype != torch.float32 or (
                 bias is not None and bias.dtype != torch.float32):
@@ -67,8 +77,16 @@ class HipLinear(torch.autograd.Function):
         _launch(x.device, _problem(M, N, K, x, x.stride(0), 1, w, K, 1, y, N,
                                    bias=None if bias is None else bias.contiguous(), alpha=alpha,
                                    relu=relu))
+        scale = alpha
+        if drop_p > 0.0:
+            if not relu or alpha != 1.0:
+                raise ValueError("the folded dropout backward needs a ReLU layer with alpha 1")
+            y, _ = torch.native_dropout(y, drop_p, True)
+            # masked_scale's factor, as torch rounds it; p = 1 drops everything
+            scale = float(torch.tensor(1.0 / (1.0 - drop_p), dtype=torch.float32)) \
+                if drop_p < 1.0 else 0.0
         ctx.save_for_backward(x, w, y if relu else None)
-        ctx.alpha, ctx.has_bias = alpha, bias is not None
+        ctx.alpha, ctx.has_bias = scale, bias is not None
         return y
 
     @staticmethod
@@ -93,7 +111,7 @@ class HipLinear(torch.autograd.Function):
                                      ones_col=K if ctx.has_bias else -1, out_col=gb))
         if problems:
             _launch(x.device, *problems)  # dx and dW + db in one launch pair
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None, None, None
 
 
 def _check_params(x, *wb):
@@ -216,9 +234,10 @@ class HipRowHeads(torch.autograd.Function):
         return tuple(grads)
 
 
-def linear(x, layer, relu=False, alpha=1.0):
-    """act(alpha * layer(x)) on the matrix cores, act = ReLU if `relu`."""
-    return HipLinear.apply(x, layer.weight, layer.bias, bool(relu), float(alpha))
+def linear(x, layer, relu=False, alpha=1.0, drop_p=0.0):
+    """act(alpha * layer(x)) on the matrix cores, act = ReLU if `relu`; then,
+    if drop_p > 0, nn.Dropout(drop_p) in training mode (ReLU layers, alpha 1)."""
+    return HipLinear.apply(x, layer.weight, layer.bias, bool(relu), float(alpha), float(drop_p))
 
 
 def heads(x, a, b, alpha=1.0):

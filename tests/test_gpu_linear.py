@@ -150,6 +150,26 @@ def test_vae_linear_backends_agree():
                               n_train_sample=16, n_test_sample=16, mode="train",
                               nll_coeff=0.5, c_coeff=10.0)
     masks, res = [], {}
+    # the ReLU masks are taken from VAE._lin, which the folded dropout path
+    # bypasses (its own test: test_vae_dropout_fold_bit_equal)
+    fold, mpvae.FOLD_DROPOUT = mpvae.FOLD_DROPOUT, False
+    try:
+        _backends_run(args, masks, res)
+    finally:
+        mpvae.FOLD_DROPOUT = fold
+    assert len(masks) == 7  # encoders 2 + 3 ReLU layers, the stacked decoder pass of 2
+    errs = {}
+    for i, (a, b) in enumerate(zip(res["hip"][0], res["torch"][0])):
+        errs[f"out{i}"] = rel_err(a.cpu(), b.cpu())
+    for k, v in res["torch"][1].items():
+        errs["param_" + k] = rel_err(res["hip"][1][k].cpu(), v.cpu())
+    record("vae_linear_hip_vs_torch", errs)
+    for k, e in errs.items():
+        assert e < LINEAR_VAE_RTOL, (k, e)
+
+
+def _backends_run(args, masks, res):
+    import mpvae
     for backend in ("hip", "torch"):
         args.mpvae_linear = backend
         torch.manual_seed(0)
@@ -181,15 +201,41 @@ def test_vae_linear_backends_agree():
         res[backend] = ([o.detach() for o in out],
                         {k: p.grad.clone() for k, p in model.named_parameters()
                          if p.grad is not None})
-    assert len(masks) == 7  # encoders 2 + 3 ReLU layers, the stacked decoder pass of 2
-    errs = {}
-    for i, (a, b) in enumerate(zip(res["hip"][0], res["torch"][0])):
-        errs[f"out{i}"] = rel_err(a.cpu(), b.cpu())
-    for k, v in res["torch"][1].items():
-        errs["param_" + k] = rel_err(res["hip"][1][k].cpu(), v.cpu())
-    record("vae_linear_hip_vs_torch", errs)
-    for k, e in errs.items():
-        assert e < LINEAR_VAE_RTOL, (k, e)
+
+
+def test_vae_dropout_fold_bit_equal():
+    """The VAE on mpv_linear with the encoders' dropout backward folded into
+    the gradient GEMMs equals the same VAE with nn.Dropout's own backward, bit
+    for bit (outputs and every parameter gradient, reference keep_prob 0.5)."""
+    import argparse
+
+    import mpvae
+    args = argparse.Namespace(feature_dim=1000, latent_dim=50, label_dim=38, z_dim=38,
+                              keep_prob=0.5, scale_coeff=1.0, residue_sigma="",
+                              n_train_sample=16, n_test_sample=16, mode="train",
+                              nll_coeff=0.5, c_coeff=10.0, mpvae_linear="hip")
+    res = {}
+    fold = mpvae.FOLD_DROPOUT
+    try:
+        for f in (True, False):
+            mpvae.FOLD_DROPOUT = f
+            torch.manual_seed(0)
+            np.random.seed(0)
+            model = mpvae.VAE(args).to(DEV).train()
+            g = torch.Generator().manual_seed(3)
+            feat = torch.randn(128, 1000, generator=g).to(DEV)
+            label = (torch.rand(128, 38, generator=g) < 0.2).float().to(DEV)
+            torch.cuda.manual_seed(9)
+            out = model(label, feat)
+            w = [torch.randn(o.shape, generator=g).to(DEV) for o in out]
+            sum((o * wi).sum() for o, wi in zip(out, w)).backward()
+            res[f] = [o.detach() for o in out] + [p.grad.clone() for p in model.parameters()
+                                                  if p.grad is not None]
+    finally:
+        mpvae.FOLD_DROPOUT = fold
+    assert len(res[True]) == len(res[False])
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("M,K,Na,Nb,alpha", [(128, 256, 50, 50, 1.3), (7, 20, 6, 3, 1.0),
@@ -243,3 +289,26 @@ def test_row_heads_match_fp64(M, n_a, K, Na, Nb):
     record(f"linear_row_heads_{M}_{n_a}_{K}", errs)
     for k, e in errs.items():
         assert e < LINEAR_RTOL, (k, e)
+
+
+@pytest.mark.parametrize("p", [0.5, 0.1, 0.9])
+@pytest.mark.parametrize("M,K,N", [(128, 1000, 256), (32, 1038, 512), (33, 17, 65)])
+def test_dropout_backward_folded_bit_equal(p, M, K, N):
+    """linear(..., drop_p=p) -- torch's dropout kernel in the forward, its
+    backward folded into the gradient GEMMs' operand load -- equals ReLU layer
+    then nn.Dropout(p) (separate masked_scale backward) bit for bit: the same
+    generator draws the same masks, and (out > 0) * 1/(1-p) reproduces
+    masked_scale + threshold_backward exactly."""
+    layer = _layer(K, N, seed=7)
+    x = torch.randn((M, K), device=DEV, requires_grad=True)
+    gy = torch.randn((M, N), device=DEV)
+
+    def run(fold):
+        torch.cuda.manual_seed(123)
+        if fold:
+            y = mpvae_linear.linear(x, layer, True, 1.0, p)
+        else:
+            y = torch.nn.functional.dropout(mpvae_linear.linear(x, layer, True, 1.0), p, True)
+        return (y.detach(),) + torch.autograd.grad(y, (x, layer.weight, layer.bias), gy)
+    for a, b in zip(run(True), run(False)):
+        assert torch.equal(a, b)

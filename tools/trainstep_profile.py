@@ -96,7 +96,10 @@ def main():
     ap.add_argument("--ops", action="store_true")
     # TrainStep's Adam: mpv_adam_step (default) or torch's fused kernel, for A/B
     ap.add_argument("--torch-adam", action="store_true")
+    # nn.Dropout's own backward kernel instead of the fold into mpv_linear
+    ap.add_argument("--no-fold-dropout", action="store_true")
     cli = ap.parse_args()
+    mpvae.FOLD_DROPOUT = not cli.no_fold_dropout
     dev = torch.device("cuda", 0)
     if cli.blas:
         torch.backends.cuda.preferred_blas_library(cli.blas)
@@ -166,6 +169,7 @@ def main():
                       "steps": cli.steps, "eager_ms": round(eager_ms, 4),
                       "phases_ms": phases, "trainstep_ms": round(ts_ms, 4),
                       "graph_ms": round(graph_ms, 4), "adam": "torch" if cli.torch_adam else "mpv_adam_step",
+                      "fold_dropout": mpvae.FOLD_DROPOUT,
                       "updates": int(ts.updates),
                       "loss_finite": bool(torch.isfinite(ts.out[0]).item()),
                       "kernels": kernels}), flush=True)

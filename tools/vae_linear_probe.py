@@ -33,6 +33,7 @@ def run(backend):
     names = {id(m): n for n, m in model.named_modules()}
     rec = []
     orig = model._lin
+    mpvae.FOLD_DROPOUT = False  # every ReLU layer through model._lin (recorded)
 
     def lin(layer, x, relu=False, alpha=1.0):
         xx = x.detach().clone()
