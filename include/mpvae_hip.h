@@ -37,7 +37,8 @@ extern "C" {
                               6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
                                  dR64 and kl;
                               7: mpv_linear_batch takes up to 4 problems
-                              8: mpv_adam_step */
+                              8: mpv_adam_step; mpv_reparam_bwd_args adds
+                                 the other consumers' mu / logvar gradients */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -267,6 +268,12 @@ typedef struct mpv_reparam_bwd_args {
   float* gmu_x;
   float* glogvar_x;
   int64_t n_x;
+  /* ABI v8: gradients of mu / logvar from their other consumers (the KL in
+   * compute_loss), added to the outputs (NULL = none) */
+  const float* gmu_add_e;
+  const float* glogvar_add_e;
+  const float* gmu_add_x;
+  const float* glogvar_add_x;
 } mpv_reparam_bwd_args;
 
 int mpv_reparam_bwd(const mpv_reparam_bwd_args* args, void* stream);

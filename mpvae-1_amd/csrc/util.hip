@@ -266,6 +266,7 @@ __global__ void reparam_fwd_kernel(mpv_reparam_args a) {
 }
 
 __global__ void reparam_bwd_kernel(mpv_reparam_bwd_args a) {
+#pragma clang fp contract(off)
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float* gz;
   const float* lv;
@@ -280,9 +281,14 @@ __global__ void reparam_bwd_kernel(mpv_reparam_bwd_args a) {
   } else {
     return;
   }
+  const float* amu = i < a.n_e ? a.gmu_add_e : a.gmu_add_x;
+  const float* alv = i < a.n_e ? a.glogvar_add_e : a.glogvar_add_x;
+  // the gradients mu / logvar also receive elsewhere (compute_loss's KL),
+  // added as autograd would add them: one rounded add (fp contract off above)
   const float g = gz ? gz[j] : 0.0f;
-  gmu[j] = g;
-  glv[j] = g * ep[j] * 0.5f * expf(0.5f * lv[j]);
+  const float r = g * ep[j] * 0.5f * expf(0.5f * lv[j]);
+  gmu[j] = amu ? g + amu[j] : g;
+  glv[j] = alv ? r + alv[j] : r;
 }
 
 // d KL / d (mu, logvar) of mpvae.py:147-148 (kl_bwd_range, mpv_common.h).

@@ -49,6 +49,9 @@ __all__ = ["VAE", "compute_loss"]
 # the encoders' dropout backward folded into mpv_linear (same values; False:
 # nn.Dropout's own backward kernel, for A/B)
 FOLD_DROPOUT = True
+# mu / logvar returned through FusedReparam (their KL gradient added in its
+# backward launch; same values; False: autograd adds them, for A/B)
+REPARAM_PASSTHROUGH = True
 
 # (attribute, in_features, out_features) in the reference's construction order
 # (mpvae.py:14-32).  The order fixes the torch init draws and the state_dict
@@ -171,7 +174,12 @@ class VAE(nn.Module):
         eps_e = self.reparam_noise(lv_e)
         mu_x, lv_x = self.feat_encode(feature)
         eps_x = self.reparam_noise(lv_x)
-        z_e, z_x = FusedReparam.apply(mu_e, lv_e, eps_e, mu_x, lv_x, eps_x)
+        # mu / logvar come back through the fused op: compute_loss's KL gradient
+        # for them is then added inside its backward launch
+        r = FusedReparam.apply(mu_e, lv_e, eps_e, mu_x, lv_x, eps_x)
+        z_e, z_x = r[:2]
+        if REPARAM_PASSTHROUGH:
+            mu_e, lv_e, mu_x, lv_x = r[2:]
         if self.linear_backend == "hip":
             # both decoders share fd_x1 / fd_x2 (mpvae.py:31-32): run them
             # once on the two inputs stacked, then the two heads on their rows

@@ -79,7 +79,9 @@ class ReparamArgs(ctypes.Structure):
 class ReparamBwdArgs(ctypes.Structure):
     _fields_ = [("gz_e", vp), ("logvar_e", vp), ("eps_e", vp), ("gmu_e", vp), ("glogvar_e", vp),
                 ("n_e", ctypes.c_int64), ("gz_x", vp), ("logvar_x", vp), ("eps_x", vp),
-                ("gmu_x", vp), ("glogvar_x", vp), ("n_x", ctypes.c_int64)]
+                ("gmu_x", vp), ("glogvar_x", vp), ("n_x", ctypes.c_int64),
+                ("gmu_add_e", vp), ("glogvar_add_e", vp), ("gmu_add_x", vp),
+                ("glogvar_add_x", vp)]
 
 
 class LabelTable(ctypes.Structure):

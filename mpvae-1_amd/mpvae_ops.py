@@ -364,7 +364,13 @@ class ProbitELBO(torch.autograd.Function):
 class FusedReparam(torch.autograd.Function):
     """z = mu + eps*exp(0.5*logvar) for the label and the feature encoder in one
     launch (mpvae.py:66-74).  eps is an input (drawn by the caller with
-    torch.randn_like, so the RNG stream matches the reference's draw order)."""
+    torch.randn_like, so the RNG stream matches the reference's draw order).
+
+    mu and logvar are also passed through as outputs: the VAE returns those
+    (same tensors' values) to the caller, so the gradient compute_loss's KL
+    sends them arrives here and is added inside mpv_reparam_bwd -- the one
+    add autograd would otherwise launch per tensor when two consumers of an
+    encoder head meet."""
 
     @staticmethod
     def forward(ctx, mu_e, lv_e, eps_e, mu_x, lv_x, eps_x):
@@ -377,18 +383,21 @@ class FusedReparam(torch.autograd.Function):
         H.check(H.load_library().mpv_reparam_fwd(a, H.stream_of(mu_e.device)), "mpv_reparam_fwd")
         ctx.save_for_backward(lv_e, eps_e, lv_x, eps_x)
         ctx.set_materialize_grads(False)
-        return z_e, z_x
+        return z_e, z_x, mu_e, lv_e, mu_x, lv_x
 
     @staticmethod
-    def backward(ctx, gz_e, gz_x):
+    def backward(ctx, gz_e, gz_x, gmu_e_in, glv_e_in, gmu_x_in, glv_x_in):
         lv_e, eps_e, lv_x, eps_x = ctx.saved_tensors
         gmu_e, glv_e = torch.empty_like(lv_e), torch.empty_like(lv_e)
         gmu_x, glv_x = torch.empty_like(lv_x), torch.empty_like(lv_x)
-        gz_e = None if gz_e is None else gz_e.contiguous()
-        gz_x = None if gz_x is None else gz_x.contiguous()
+        c = lambda g: None if g is None else _f32(g, "reparam gradient")
+        gz_e, gz_x = c(gz_e), c(gz_x)
+        gmu_e_in, glv_e_in, gmu_x_in, glv_x_in = (c(g) for g in (gmu_e_in, glv_e_in, gmu_x_in,
+                                                                  glv_x_in))
         a = H.ReparamBwdArgs(H.ptr(gz_e), H.ptr(lv_e), H.ptr(eps_e), H.ptr(gmu_e), H.ptr(glv_e),
                              lv_e.numel(), H.ptr(gz_x), H.ptr(lv_x), H.ptr(eps_x), H.ptr(gmu_x),
-                             H.ptr(glv_x), lv_x.numel())
+                             H.ptr(glv_x), lv_x.numel(), H.ptr(gmu_e_in), H.ptr(glv_e_in),
+                             H.ptr(gmu_x_in), H.ptr(glv_x_in))
         H.check(H.load_library().mpv_reparam_bwd(a, H.stream_of(lv_e.device)), "mpv_reparam_bwd")
         return gmu_e, glv_e, None, gmu_x, glv_x, None
 

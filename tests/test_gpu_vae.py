@@ -292,3 +292,27 @@ def test_native_adam_matches_torch_fused_adam():
     # the state is torch's own: a state_dict round trip restores it
     sd = copy.deepcopy(mine.state_dict())
     assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+def test_fused_reparam_passthrough_grads_bit_equal():
+    """FusedReparam's mu / logvar pass-through outputs: a gradient reaching
+    them (compute_loss's KL) is added inside mpv_reparam_bwd, and equals, bit
+    for bit, autograd adding it to the reparameterisation gradient when the
+    original mu / logvar tensors are used instead."""
+    from mpvae_ops import FusedReparam
+    torch.manual_seed(4)
+    shp = [(128, 50), (128, 50)]
+    leaves = [torch.randn(s, device=DEV, requires_grad=True) for s in shp + shp]
+    mu_e, lv_e, mu_x, lv_x = leaves
+    eps_e, eps_x = torch.randn(shp[0], device=DEV), torch.randn(shp[1], device=DEV)
+    w = [torch.randn(shp[0], device=DEV) for _ in range(6)]
+
+    def grads(passthrough):
+        h = [t * 1.0 for t in leaves]  # non-leaf heads, as the encoders' outputs
+        out = FusedReparam.apply(h[0], h[1], eps_e, h[2], h[3], eps_x)
+        z_e, z_x = out[:2]
+        m = out[2:] if passthrough else h
+        loss = sum((a * b).sum() for a, b in zip((z_e, z_x) + tuple(m), w))
+        return torch.autograd.grad(loss, leaves)
+    for a, b in zip(grads(True), grads(False)):
+        assert torch.equal(a, b)

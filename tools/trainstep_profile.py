@@ -98,8 +98,11 @@ def main():
     ap.add_argument("--torch-adam", action="store_true")
     # nn.Dropout's own backward kernel instead of the fold into mpv_linear
     ap.add_argument("--no-fold-dropout", action="store_true")
+    # autograd's adds of the encoder heads' two gradients instead of mpv_reparam_bwd's
+    ap.add_argument("--no-passthrough", action="store_true")
     cli = ap.parse_args()
     mpvae.FOLD_DROPOUT = not cli.no_fold_dropout
+    mpvae.REPARAM_PASSTHROUGH = not cli.no_passthrough
     dev = torch.device("cuda", 0)
     if cli.blas:
         torch.backends.cuda.preferred_blas_library(cli.blas)
@@ -170,6 +173,7 @@ def main():
                       "phases_ms": phases, "trainstep_ms": round(ts_ms, 4),
                       "graph_ms": round(graph_ms, 4), "adam": "torch" if cli.torch_adam else "mpv_adam_step",
                       "fold_dropout": mpvae.FOLD_DROPOUT,
+                      "reparam_passthrough": mpvae.REPARAM_PASSTHROUGH,
                       "updates": int(ts.updates),
                       "loss_finite": bool(torch.isfinite(ts.out[0]).item()),
                       "kernels": kernels}), flush=True)
