@@ -38,7 +38,8 @@ extern "C" {
                                  dR64 and kl;
                               7: mpv_linear_batch takes up to 4 problems
                               8: mpv_adam_step; mpv_reparam_bwd_args adds
-                                 the other consumers' mu / logvar gradients */
+                                 the other consumers' mu / logvar gradients;
+                                 mpv_linear_args second reduction segment */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -307,6 +308,13 @@ typedef struct mpv_linear_args {
   float* out;
   int64_t out_si;
   float* out_col;    /* (M), with ones_col */
+  /* ABI v8: optional second reduction segment -- for r >= R1 the sum reads
+   * A = a2 (row stride a2_si, reduction stride a_sr) and B = b2 (B's
+   * strides) at index r - R1; a2 = b2 = NULL: one segment.  No a_mask. */
+  const float* a2;
+  int64_t a2_si;
+  const float* b2;
+  int64_t R1;
 } mpv_linear_args;
 
 size_t mpv_linear_workspace_bytes(int64_t M, int64_t N, int64_t R);

@@ -19,6 +19,8 @@
 // reduction rows per LDS stage (64 measured no faster: 0.46 vs 0.36 ms for
 // the 43 GEMMs of a C3 training step); the next stage's global loads are
 // issued before the current stage's MFMAs (register double buffer).
+// A problem may have a second reduction segment (other A and B pointers for
+// reduction indices >= R1): the two heads' dx of one input as one GEMM.
 // Independent GEMMs (a layer's dx and dW; both heads of an encoder, or of
 // the stacked decoder, with their gradients) go in one launch: up to
 // kLinMaxProb problems, told apart by blockIdx.z ranges.
@@ -52,6 +54,12 @@ struct LinParams {
   float* out_col;
   float* part;    // (nsplit, M, N) chunk partials, null: direct epilogue
   int64_t chunk;  // reduction rows per split
+  // second reduction segment (a2 != null): reduction index r >= R1 reads
+  // A = a2 (row stride a2_si) and B = b2 (B's strides) at r - R1
+  const float* a2;
+  int64_t a2_si;
+  const float* b2;
+  int64_t R1;
 };
 
 // kLinPer elements of a 64-row x 64-reduction operand tile, mapped so that
@@ -83,8 +91,10 @@ MPV_DEV void lin_load(const LinParams& p, const LinSlot& sl, int64_t row0, int64
       if (!IS_A && row == p.ones_col) {
         x = 1.0f;
       } else {
-        const int64_t o = row * s_row + r * s_red;
-        x = src[o];
+        const bool seg2 = (IS_A ? p.a2 : p.b2) != nullptr && r >= p.R1;
+        const int64_t o = seg2 ? row * (IS_A ? p.a2_si : s_row) + (r - p.R1) * s_red
+                               : row * s_row + r * s_red;
+        x = seg2 ? (IS_A ? p.a2 : p.b2)[o] : src[o];
         if (IS_A) {
           // ReLU backward: torch's threshold_backward passes the gradient
           // where the layer output is > 0 (NaN outputs block it)
@@ -287,6 +297,13 @@ int mpv_linear_batch(const mpv_linear_args* args, int n, void* workspace, size_t
     p.out = a->out;
     p.out_si = a->out_si;
     p.out_col = a->out_col;
+    MPV_REQUIRE((a->a2 == nullptr) == (a->b2 == nullptr) &&
+                    (a->a2 == nullptr || (a->a_mask == nullptr && a->R1 >= 0 && a->R1 <= a->R)),
+                "linear: a second segment needs a2 and b2, no mask, 0 <= R1 <= R (problem %d)", k);
+    p.a2 = a->a2;
+    p.a2_si = a->a2_si;
+    p.b2 = a->b2;
+    p.R1 = a->a2 != nullptr ? a->R1 : a->R;
     p.part = pl.nsplit > 1 ? reinterpret_cast<float*>(ws + off) : nullptr;
     p.chunk = pl.chunk;
     off += pl.part_bytes;

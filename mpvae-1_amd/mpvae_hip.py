@@ -100,7 +100,8 @@ class LinearArgs(ctypes.Structure):
                 ("a_scale", ctypes.c_float), ("b", vp), ("b_sj", ctypes.c_int64),
                 ("b_sr", ctypes.c_int64), ("ones_col", ctypes.c_int64), ("bias", vp),
                 ("alpha", ctypes.c_float), ("relu", ctypes.c_int), ("out", vp),
-                ("out_si", ctypes.c_int64), ("out_col", vp)]
+                ("out_si", ctypes.c_int64), ("out_col", vp), ("a2", vp),
+                ("a2_si", ctypes.c_int64), ("b2", vp), ("R1", ctypes.c_int64)]
 
 
 ADAM_MAX_TENSORS = 32

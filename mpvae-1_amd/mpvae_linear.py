@@ -22,11 +22,14 @@ import mpvae_hip as H
 
 
 def _problem(M, N, R, a, a_si, a_sr, b, b_sj, b_sr, out, out_si, *, a_mask=None, a_scale=1.0,
-             ones_col=-1, out_col=None, bias=None, alpha=1.0, relu=False):
+             ones_col=-1, out_col=None, bias=None, alpha=1.0, relu=False, seg2=None):
+    """seg2 = (R1, a2, a2_si, b2): reduction indices >= R1 read a2 / b2."""
+    R1, a2, a2_si, b2 = seg2 if seg2 is not None else (0, None, 0, None)
     return H.LinearArgs(M=M, N=N, R=R, a=H.ptr(a), a_si=a_si, a_sr=a_sr, a_mask=H.ptr(a_mask),
                         a_scale=a_scale, b=H.ptr(b), b_sj=b_sj, b_sr=b_sr, ones_col=ones_col,
                         bias=H.ptr(bias), alpha=alpha, relu=int(bool(relu)), out=H.ptr(out),
-                        out_si=out_si, out_col=H.ptr(out_col))
+                        out_si=out_si, out_col=H.ptr(out_col), a2=H.ptr(a2), a2_si=a2_si,
+                        b2=H.ptr(b2), R1=R1)
 
 
 def _launch(device, *problems):
@@ -37,6 +40,10 @@ def _launch(device, *problems):
     ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
     H.check(lib.mpv_linear_batch(arr, len(problems), H.ptr(ws), nbytes, H.stream_of(device)),
             "mpv_linear")
+
+
+# the two heads' dx as one two-segment GEMM (False: two GEMMs and an add, A/B)
+HEADS_DX_ONE_GEMM = True
 
 
 def _rows(x):
@@ -156,14 +163,23 @@ class HipLinearHeads(torch.autograd.Function):
         dev = x.device
         need = ctx.needs_input_grad
         grads = [None] * 6
-        problems, dxs = [], []
+        problems = []
+        ga, gb_ = ga.contiguous(), gb_.contiguous()
+        dxs = []
+        if need[0] and not HEADS_DX_ONE_GEMM:
+            for w, g in ((wa, ga), (wb, gb_)):
+                dxs.append(torch.empty((M, K), dtype=torch.float32, device=dev))
+                problems.append(_problem(M, K, w.shape[0], g, w.shape[0], 1, w, 1, K, dxs[-1], K,
+                                         a_scale=ctx.alpha))
+        elif need[0]:
+            # dx = ga Wa + gb Wb: one GEMM over the two heads' outputs (two
+            # reduction segments), no separate sum
+            Na, Nb = wa.shape[0], wb.shape[0]
+            grads[0] = torch.empty((M, K), dtype=torch.float32, device=dev)
+            problems.append(_problem(M, K, Na + Nb, ga, Na, 1, wa, 1, K, grads[0], K,
+                                     a_scale=ctx.alpha, seg2=(Na, gb_, Nb, wb)))
         for k, (w, g) in enumerate(((wa, ga), (wb, gb_))):
-            g = g.contiguous()
             N = w.shape[0]
-            if need[0]:
-                dx = torch.empty((M, K), dtype=torch.float32, device=dev)
-                problems.append(_problem(M, K, N, g, N, 1, w, 1, K, dx, K, a_scale=ctx.alpha))
-                dxs.append(dx)
             if need[1 + 2 * k] or need[2 + 2 * k]:
                 hb = ctx.has_bias[k]
                 gw = torch.empty((N, K), dtype=torch.float32, device=dev)
@@ -174,7 +190,7 @@ class HipLinearHeads(torch.autograd.Function):
                 grads[1 + 2 * k], grads[2 + 2 * k] = gw, gbias
         if problems:
             _launch(dev, *problems)
-        if need[0]:
+        if dxs:
             grads[0] = dxs[0].add_(dxs[1])
         return tuple(grads)
 

@@ -110,3 +110,8 @@ def test_linear_host_checks():
                        b_sr=1, ones_col=-1, alpha=1.0, out=fake, out_si=256)
     assert lib.mpv_linear(ctypes.byref(big), None, 0, None) == 1  # no workspace for the partials
     assert b"workspace" in lib.mpv_last_error()
+    # a second reduction segment needs both operands and no mask (ABI v8)
+    half = H.LinearArgs(M=4, N=4, R=4, a=fake, a_si=4, a_sr=1, b=fake, b_sj=4, b_sr=1,
+                        ones_col=-1, alpha=1.0, out=fake, out_si=4, a2=fake, a2_si=4, R1=2)
+    assert lib.mpv_linear(ctypes.byref(half), None, 0, None) == 1
+    assert b"second segment" in lib.mpv_last_error()

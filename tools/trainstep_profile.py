@@ -100,7 +100,11 @@ def main():
     ap.add_argument("--no-fold-dropout", action="store_true")
     # autograd's adds of the encoder heads' two gradients instead of mpv_reparam_bwd's
     ap.add_argument("--no-passthrough", action="store_true")
+    # the encoder heads' dx as two GEMMs and an add instead of one two-segment GEMM
+    ap.add_argument("--heads-dx-two", action="store_true")
     cli = ap.parse_args()
+    import mpvae_linear
+    mpvae_linear.HEADS_DX_ONE_GEMM = not cli.heads_dx_two
     mpvae.FOLD_DROPOUT = not cli.no_fold_dropout
     mpvae.REPARAM_PASSTHROUGH = not cli.no_passthrough
     dev = torch.device("cuda", 0)
