@@ -352,6 +352,7 @@ typedef struct mpv_adam_args {
   mpv_adam_tensor t[MPV_ADAM_MAX_TENSORS];
   double lr, beta1, beta2, weight_decay, eps;
   const float* found_inf;
+  int64_t* updates;  /* NULL, or a counter incremented when the update is applied */
 } mpv_adam_args;
 
 int mpv_adam_step(const mpv_adam_args* args, void* stream);

@@ -30,6 +30,7 @@ struct AdamBatch {
   int n;
   double lr, beta1, beta2, weight_decay, eps;
   const float* found_inf;
+  int64_t* updates;
 };
 
 template <typename T>
@@ -71,6 +72,7 @@ MPV_DEV void adam_block(const mpv_adam_tensor& t, int64_t e0, const AdamBatch& a
 __global__ __launch_bounds__(kAdamThreads) void adam_kernel(AdamBatch a) {
   if (a.found_inf != nullptr && *a.found_inf == 1.0f) return;
   const int64_t blk = blockIdx.x;
+  if (a.updates != nullptr && blk == 0 && threadIdx.x == 0) a.updates[0] += 1;  // applied
   int q = 0;
   for (int k = 1; k < a.n; ++k)
     if (blk >= a.boff[k]) q = k;
@@ -98,6 +100,7 @@ extern "C" int mpv_adam_step(const mpv_adam_args* args, void* stream) {
   a.weight_decay = args->weight_decay;
   a.eps = args->eps;
   a.found_inf = args->found_inf;
+  a.updates = args->updates;
   a.boff[0] = 0;
   for (int k = 0; k < args->n; ++k) {
     const mpv_adam_tensor& t = args->t[k];
@@ -110,6 +113,7 @@ extern "C" int mpv_adam_step(const mpv_adam_args* args, void* stream) {
   for (int k = args->n; k < MPV_ADAM_MAX_TENSORS; ++k) a.boff[k + 1] = a.boff[k];
   const int64_t blocks = a.boff[args->n];
   MPV_REQUIRE(blocks < (1ll << 31), "adam: too many elements");
+  MPV_REQUIRE(blocks > 0 || args->updates == nullptr, "adam: an update counter needs a tensor");
   if (blocks == 0) return MPV_OK;
   MPV_LAUNCH("adam", adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0,
              as_stream(stream), a);

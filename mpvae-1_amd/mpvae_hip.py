@@ -117,7 +117,7 @@ class AdamArgs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("t", AdamTensor * ADAM_MAX_TENSORS),
                 ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("weight_decay", ctypes.c_double), ("eps", ctypes.c_double),
-                ("found_inf", vp)]
+                ("found_inf", vp), ("updates", vp)]
 
 
 class FairArgs(ctypes.Structure):

@@ -70,14 +70,15 @@ def _native_adam(opt):
     return True
 
 
-def adam_step(opt, found_inf):
+def adam_step(opt, found_inf, updates=None):
     """optimizer.step() of a fused torch.optim.Adam in one mpv_adam_step launch
     per parameter group (csrc/adam.hip) instead of torch's multi-tensor kernel,
     which runs the VAE's 1.5 M parameters on ~25 workgroups (DESIGN.md
     section 11).  Same state (``step``, ``exp_avg``, ``exp_avg_sq`` in
     ``opt.state``), same step-count protocol as torch's capturable fused path
     (+1 before, -found_inf after), same per-element arithmetic; nothing is
-    written when ``found_inf`` is 1."""
+    written when ``found_inf`` is 1.  ``updates`` (an int64 device scalar, or
+    None) counts the applied updates, inside the same launch."""
     import mpvae_hip as H
     lib = H.load_library()
     for g in opt.param_groups:
@@ -96,7 +97,8 @@ def adam_step(opt, found_inf):
         for c in range(0, len(params), H.ADAM_MAX_TENSORS):
             a = H.AdamArgs(n=0, lr=float(g["lr"]), beta1=float(beta1), beta2=float(beta2),
                            weight_decay=float(g["weight_decay"]), eps=float(g["eps"]),
-                           found_inf=H.ptr(found_inf))
+                           found_inf=H.ptr(found_inf), updates=H.ptr(updates))
+            updates = None  # counted once per step
             for p in params[c:c + H.ADAM_MAX_TENSORS]:
                 st = opt.state[p]
                 ts = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
@@ -198,6 +200,9 @@ class TrainStep:
                 by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
         for grads in by_dtype.values():
             torch._amp_foreach_non_finite_check_and_unscale_(grads, self.found_inf, self._one)
+        if self.native_adam and any(p.grad is not None for p in self.params):
+            adam_step(self.opt, self.found_inf, self.updates)
+            return res
         if self.native_adam:
             adam_step(self.opt, self.found_inf)
         else:
