@@ -5,12 +5,16 @@ and its autograd) over one synthetic batch, with the probit noise generated on
 the device (philox mode), inputs resident in HBM.  Metric (BASELINE.json):
 probit MC label-samples/s = n_sample x B x L per step, whole job.
 
-Default workload (north star): C4 -- B=512, n_sample=4096 per GPU, L=z=1024.
-With --gpus N each rank evaluates its own 4096 samples of an n_sample=4096*N
-estimate (weak scaling), exchanging only the exact log-sum-exp statistics and
-gradient sums (mpvae_dist.py).
+Default workload (north star): C4 -- B=512, n_sample=4096, L=z=1024.  With
+--gpus N the n_sample axis of that one estimate is split over the N ranks
+(strong scaling, the default: 4096/N samples per GPU, the north star's "scaling
+at 8 GPUs" of the (512, 4096, 1024) problem), exchanging only the exact
+log-sum-exp statistics and gradient sums (mpvae_dist.py).  --scaling weak
+gives every rank its own 4096 samples of an n_sample = 4096*N estimate.
+--n-sample overrides the config's n_sample (e.g. 512: one rank's share at N=8,
+timed on one GPU with MPVAE_FORCE_DIST=1 to see the fixed costs).
 
-    python bench.py [--gpus N --steps K --warmup W --config c4|c2|c3|c5]
+    python bench.py [--gpus N --steps K --warmup W --config c4|c2|c3|c5 --scaling strong|weak]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 ``python bench.py --gpus N`` (N > 1, no WORLD_SIZE in the environment) starts
@@ -45,12 +49,13 @@ PEAKS = {"f16x3": (F16_MFMA_PEAK / 3.0, "f16x3 MFMA: dense f16 peak / 3"),
          "f32": (FP32_MFMA_PEAK, "f32 MFMA")}
 HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec
 
-# name: (L, z, B, n_sample per GPU (weak) or total (strong), d, nll_coeff, c_coeff, scaling)
+# name: (L, z, B, n_sample (total under strong scaling, per GPU under weak), d,
+#        nll_coeff, c_coeff)
 CONFIGS = {
-    "c2": (38, 38, 128, 1000, 50, 0.5, 10.0, "weak"),
-    "c3": (81, 81, 256, 2000, 50, 0.1, 200.0, "weak"),
-    "c4": (1024, 1024, 512, 4096, 50, 0.1, 200.0, "weak"),
-    "c5": (4096, 4096, 512, 8192, 50, 0.1, 200.0, "strong"),
+    "c2": (38, 38, 128, 1000, 50, 0.5, 10.0),
+    "c3": (81, 81, 256, 2000, 50, 0.1, 200.0),
+    "c4": (1024, 1024, 512, 4096, 50, 0.1, 200.0),
+    "c5": (4096, 4096, 512, 8192, 50, 0.1, 200.0),
 }
 
 
@@ -286,6 +291,11 @@ def main():
     # its Philox key a device tensor the step advances (mpv_noise_philox*_dev);
     # per-kernel times (roofline) come from an eager pass of the same step
     ap.add_argument("--graph", action="store_true")
+    # strong (default): the config's n_sample split over the ranks; weak: n_sample
+    # per rank (n_sample * N in total)
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--n-sample", type=int, default=None,
+                    help="override the config's n_sample (train mode)")
     cli = ap.parse_args()
 
     if mpvae_launch.needs_spawn(cli.gpus):
@@ -298,11 +308,16 @@ def main():
     if world != cli.gpus:
         log(f"warning: --gpus {cli.gpus} but WORLD_SIZE {world}; using {world}")
     device = torch.device("cuda", local)
-    L, z, B, S, d, nllc, cc, scaling = CONFIGS[cli.config]
+    L, z, B, S, d, nllc, cc = CONFIGS[cli.config]
+    scaling = cli.scaling
+    if cli.n_sample is not None:
+        S = cli.n_sample
     if cli.mode == "eval":
         S = cli.eval_samples
     S_total = S * world if scaling == "weak" else S
-    S_local = S if scaling == "weak" else S // world
+    # this rank's share (mpvae_dist.split_samples: the first S % world ranks
+    # take one more; the roofline uses rank 0's)
+    S_local = S if scaling == "weak" else S // world + (1 if S % world else 0)
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S_total,
                               n_test_sample=S_total, mode="train" if cli.mode == "train" else "test",
                               nll_coeff=nllc, c_coeff=cc,

@@ -32,14 +32,18 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 8  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+#define MPV_ABI_VERSION 9  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
                               5: T rows padded to roundup(L, 4) floats;
                               6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
                                  dR64 and kl;
                               7: mpv_linear_batch takes up to 4 problems
                               8: mpv_adam_step; mpv_reparam_bwd_args adds
                                  the other consumers' mu / logvar gradients;
-                                 mpv_linear_args second reduction segment */
+                                 mpv_linear_args second reduction segment;
+                              9: mpv_adam_step reads the step count without
+                                 advancing it (mpv_adam_finish does, with the
+                                 update counter and a device StepLR); lr may
+                                 live in device memory */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -331,11 +335,14 @@ int mpv_linear_batch(const mpv_linear_args* args, int n, void* workspace, size_t
 /* One Adam update over up to MPV_ADAM_MAX_TENSORS parameter tensors, fp32 and
  * fp64 mixed, in one launch; replaces optimizer.step() of
  * torch.optim.Adam(params, lr, betas, eps, weight_decay) (fairsoft_train.py:57,
- * :146) inside mpvae_step.TrainStep, with torch's fused-Adam arithmetic
- * (L2 weight decay, no amsgrad / maximize).  `step` is the tensor's device
- * step count, already incremented for this update (torch's capturable
- * protocol); bias corrections come from it.  found_inf (may be NULL): when
- * *found_inf == 1 nothing is written. */
+ * :146; fairsoft_jaccard.py:64-65) inside mpvae_step.TrainStep, with torch's
+ * fused-Adam arithmetic (L2 weight decay, no amsgrad / maximize).  `step` is
+ * the tensor's device step count BEFORE this update: the bias corrections use
+ * step + 1 (the float add torch's capturable protocol performs), and the count
+ * itself is advanced afterwards by mpv_adam_finish.  found_inf (may be NULL):
+ * when *found_inf == 1 nothing is written.  lr_dev (may be NULL): the learning
+ * rate is read from device memory (a StepLR that mpv_adam_finish decays)
+ * instead of `lr`. */
 #define MPV_ADAM_MAX_TENSORS 32
 typedef struct mpv_adam_tensor {
   void* param;
@@ -352,17 +359,41 @@ typedef struct mpv_adam_args {
   mpv_adam_tensor t[MPV_ADAM_MAX_TENSORS];
   double lr, beta1, beta2, weight_decay, eps;
   const float* found_inf;
-  int64_t* updates;  /* NULL, or a counter incremented when the update is applied */
+  const double* lr_dev;  /* NULL, or this group's device learning rate */
 } mpv_adam_args;
 
 int mpv_adam_step(const mpv_adam_args* args, void* stream);
+
+/* After the mpv_adam_step launches of one optimizer step (one launch, one
+ * workgroup): every step count += 1 - found_inf (torch's +1 then -found_inf);
+ * the applied-update counter += 1 - found_inf (the reference's
+ * succses_updates, fairsoft_train.py:146); and, when n_lr > 0, the
+ * scheduler step the reference takes after an applied update only
+ * (fairsoft_train.py:142-145) for torch.optim.lr_scheduler.StepLR
+ * (fairsoft_jaccard.py:67-68): last_epoch += 1, and if last_epoch is a
+ * non-zero multiple of step_size (fmod, as Python's % for a float step_size)
+ * every lr[g] *= gamma in double -- the chainable form torch's StepLR.get_lr
+ * uses, so the device lr equals torch's bit for bit. */
+#define MPV_ADAM_FINISH_MAX 256
+typedef struct mpv_adam_finish_args {
+  int n_steps;
+  float* steps[MPV_ADAM_FINISH_MAX];
+  const float* found_inf; /* NULL: the update was applied */
+  int64_t* updates;       /* NULL, or the applied-update counter */
+  int n_lr;               /* 0: no scheduler */
+  double* lr;             /* n_lr device learning rates (one per param group) */
+  int64_t* last_epoch;    /* the scheduler's device last_epoch */
+  double step_size, gamma;
+} mpv_adam_finish_args;
+
+int mpv_adam_finish(const mpv_adam_finish_args* args, void* stream);
 
 /* ------------------------------------------------------------ measurement */
 /* When enabled, every kernel launch of the library is bracketed by a pair of
  * HIP events on the launch stream (bench.py's per-kernel roofline timing).
  * Kernel names: noise_philox, probit_fwd, fwd_combine, finalize, bwd_coef,
  * bwd_elem, dR_gemm, sum_slabs, convert, bstat_combine, reparam_fwd,
- * reparam_bwd, kl_bwd, linear, adam.  Query synchronises the recorded events. */
+ * reparam_bwd, kl_bwd, linear, adam, adam_finish.  Query synchronises the recorded events. */
 int mpv_timing_enable(int on);
 int mpv_timing_reset(void);
 int mpv_timing_query(const char* kernel, int64_t* launches, double* total_ms);

@@ -10,8 +10,17 @@
 // tensors in the same launch.  Per element the arithmetic is torch's own
 // (at::native adam_math, ADAM_MODE::ORIGINAL, no amsgrad / maximize / grad
 // scale): the same mixed double / opmath expressions in the same order, the
-// bias corrections from the (already incremented) device step count, and the
-// whole update skipped when *found_inf == 1.
+// bias corrections from the device step count + 1 (torch's capturable
+// protocol adds the 1 in a launch of its own first), and the whole update
+// skipped when *found_inf == 1.  FP contraction is the compiler's default for
+// device code (fast), as in torch's ROCm build of the same expressions: the
+// parameters and moments equal torch's fused Adam bit for bit
+// (tests/test_gpu_vae.py asserts torch.equal).
+//
+// adam_finish then advances the step counts, the applied-update counter and
+// the reference's StepLR (fairsoft_jaccard.py:67-68, stepped after an applied
+// update only, fairsoft_train.py:142-145) in one single-workgroup launch: the
+// update kernel reads the counts and the lr, so they cannot change inside it.
 #include <cmath>
 
 #include "abi_util.h"
@@ -30,26 +39,27 @@ struct AdamBatch {
   int n;
   double lr, beta1, beta2, weight_decay, eps;
   const float* found_inf;
-  int64_t* updates;
+  const double* lr_dev;
 };
 
 template <typename T>
-MPV_DEV void adam_elem(T& param, T grad, T& exp_avg, T& exp_avg_sq, const AdamBatch& a, T bc1,
-                       T bc2s) {
+MPV_DEV void adam_elem(T& param, T grad, T& exp_avg, T& exp_avg_sq, const AdamBatch& a, double lr,
+                       T bc1, T bc2s) {
   // adam_math with opmath_t = T: the double hyper-parameters promote each
   // expression to double, the result is stored back to T
   if (a.weight_decay != 0) grad += param * a.weight_decay;
   exp_avg = a.beta1 * exp_avg + (1 - a.beta1) * grad;
   exp_avg_sq = a.beta2 * exp_avg_sq + (1 - a.beta2) * grad * grad;
-  const T step_size = a.lr / bc1;
+  const T step_size = lr / bc1;
   const T denom = (std::sqrt(exp_avg_sq) / bc2s) + a.eps;
   param -= step_size * exp_avg / denom;
 }
 
 template <typename T>
-MPV_DEV void adam_block(const mpv_adam_tensor& t, int64_t e0, const AdamBatch& a) {
-  // bias corrections in double from the float step count, then to T
-  const float step = *t.step;
+MPV_DEV void adam_block(const mpv_adam_tensor& t, int64_t e0, const AdamBatch& a, double lr) {
+  // bias corrections in double from the float step count, then to T; the
+  // count is this update's (torch's foreach_add of 1.0 in float, done here)
+  const float step = *t.step + 1.0f;
   const T bc1 = (T)(1 - ::pow(a.beta1, step));
   const T bc2s = (T)std::sqrt(1 - ::pow(a.beta2, step));
   T* p = reinterpret_cast<T*>(t.param);
@@ -61,7 +71,7 @@ MPV_DEV void adam_block(const mpv_adam_tensor& t, int64_t e0, const AdamBatch& a
     const int64_t e = e0 + k * kAdamThreads + threadIdx.x;
     if (e < t.numel) {
       T pe = p[e], me = m[e], ve = v[e];
-      adam_elem<T>(pe, g[e], me, ve, a, bc1, bc2s);
+      adam_elem<T>(pe, g[e], me, ve, a, lr, bc1, bc2s);
       p[e] = pe;
       m[e] = me;
       v[e] = ve;
@@ -72,16 +82,41 @@ MPV_DEV void adam_block(const mpv_adam_tensor& t, int64_t e0, const AdamBatch& a
 __global__ __launch_bounds__(kAdamThreads) void adam_kernel(AdamBatch a) {
   if (a.found_inf != nullptr && *a.found_inf == 1.0f) return;
   const int64_t blk = blockIdx.x;
-  if (a.updates != nullptr && blk == 0 && threadIdx.x == 0) a.updates[0] += 1;  // applied
+  const double lr = a.lr_dev != nullptr ? *a.lr_dev : a.lr;
   int q = 0;
   for (int k = 1; k < a.n; ++k)
     if (blk >= a.boff[k]) q = k;
   const mpv_adam_tensor& t = a.t[q];
   const int64_t e0 = (blk - a.boff[q]) * kAdamBlock;
   if (t.is_f64)
-    adam_block<double>(t, e0, a);
+    adam_block<double>(t, e0, a, lr);
   else
-    adam_block<float>(t, e0, a);
+    adam_block<float>(t, e0, a, lr);
+}
+
+struct FinishBatch {
+  float* steps[MPV_ADAM_FINISH_MAX];
+  int n_steps, n_lr;
+  const float* found_inf;
+  int64_t* updates;
+  double* lr;
+  int64_t* last_epoch;
+  double step_size, gamma;
+};
+
+__global__ __launch_bounds__(MPV_ADAM_FINISH_MAX) void adam_finish_kernel(FinishBatch a) {
+  const float f = a.found_inf != nullptr ? *a.found_inf : 0.0f;
+  const int i = threadIdx.x;
+  // torch: step += 1 (before the update), step -= found_inf (after it)
+  if (i < a.n_steps) a.steps[i][0] = (a.steps[i][0] + 1.0f) - f;
+  if (i != 0 || f == 1.0f) return;
+  if (a.updates != nullptr) a.updates[0] += 1;
+  if (a.n_lr == 0) return;
+  // StepLR.step() -> get_lr(): chainable form, lr * gamma when last_epoch is
+  // a non-zero multiple of step_size (Python's % on a float step_size)
+  const int64_t e = ++a.last_epoch[0];
+  if (e != 0 && ::fmod((double)e, a.step_size) == 0.0)
+    for (int g = 0; g < a.n_lr; ++g) a.lr[g] = a.lr[g] * a.gamma;
 }
 
 }  // namespace
@@ -100,7 +135,7 @@ extern "C" int mpv_adam_step(const mpv_adam_args* args, void* stream) {
   a.weight_decay = args->weight_decay;
   a.eps = args->eps;
   a.found_inf = args->found_inf;
-  a.updates = args->updates;
+  a.lr_dev = args->lr_dev;
   a.boff[0] = 0;
   for (int k = 0; k < args->n; ++k) {
     const mpv_adam_tensor& t = args->t[k];
@@ -113,9 +148,34 @@ extern "C" int mpv_adam_step(const mpv_adam_args* args, void* stream) {
   for (int k = args->n; k < MPV_ADAM_MAX_TENSORS; ++k) a.boff[k + 1] = a.boff[k];
   const int64_t blocks = a.boff[args->n];
   MPV_REQUIRE(blocks < (1ll << 31), "adam: too many elements");
-  MPV_REQUIRE(blocks > 0 || args->updates == nullptr, "adam: an update counter needs a tensor");
   if (blocks == 0) return MPV_OK;
   MPV_LAUNCH("adam", adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0,
              as_stream(stream), a);
   return check_launch("adam");
+}
+
+extern "C" int mpv_adam_finish(const mpv_adam_finish_args* args, void* stream) {
+  MPV_REQUIRE(args != nullptr && args->n_steps >= 0 && args->n_steps <= MPV_ADAM_FINISH_MAX,
+              "adam_finish: 0..%d step counts per launch", MPV_ADAM_FINISH_MAX);
+  MPV_REQUIRE(args->n_lr >= 0, "adam_finish: bad n_lr");
+  MPV_REQUIRE(args->n_lr == 0 || (args->lr != nullptr && args->last_epoch != nullptr &&
+                                  args->step_size > 0.0),
+              "adam_finish: a scheduler needs lr, last_epoch and step_size > 0");
+  FinishBatch a;
+  a.n_steps = args->n_steps;
+  for (int k = 0; k < args->n_steps; ++k) {
+    MPV_REQUIRE(args->steps[k] != nullptr, "adam_finish: NULL step count %d", k);
+    a.steps[k] = args->steps[k];
+  }
+  a.found_inf = args->found_inf;
+  a.updates = args->updates;
+  a.n_lr = args->n_lr;
+  a.lr = args->lr;
+  a.last_epoch = args->last_epoch;
+  a.step_size = args->step_size;
+  a.gamma = args->gamma;
+  if (a.n_steps == 0 && a.updates == nullptr && a.n_lr == 0) return MPV_OK;
+  MPV_LAUNCH("adam_finish", adam_finish_kernel, dim3(1), dim3(MPV_ADAM_FINISH_MAX), 0,
+             as_stream(stream), a);
+  return check_launch("adam_finish");
 }

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -117,7 +117,17 @@ class AdamArgs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("t", AdamTensor * ADAM_MAX_TENSORS),
                 ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("weight_decay", ctypes.c_double), ("eps", ctypes.c_double),
-                ("found_inf", vp), ("updates", vp)]
+                ("found_inf", vp), ("lr_dev", vp)]
+
+
+ADAM_FINISH_MAX = 256
+
+
+class AdamFinishArgs(ctypes.Structure):
+    """mpv_adam_finish_args: step counts, update counter and StepLR (adam.hip)."""
+    _fields_ = [("n_steps", ctypes.c_int), ("steps", vp * ADAM_FINISH_MAX), ("found_inf", vp),
+                ("updates", vp), ("n_lr", ctypes.c_int), ("lr", vp), ("last_epoch", vp),
+                ("step_size", ctypes.c_double), ("gamma", ctypes.c_double)]
 
 
 class FairArgs(ctypes.Structure):
@@ -160,6 +170,7 @@ SIGNATURES = {
     "mpv_linear_batch": (ctypes.c_int, [ctypes.POINTER(LinearArgs), ctypes.c_int, vp,
                                         ctypes.c_size_t, vp]),
     "mpv_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamArgs), vp]),
+    "mpv_adam_finish": (ctypes.c_int, [ctypes.POINTER(AdamFinishArgs), vp]),
     "mpv_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "mpv_timing_reset": (ctypes.c_int, []),
     "mpv_timing_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64),
@@ -235,7 +246,8 @@ def require_gpu(*tensors):
 
 KERNELS = ["noise_philox", "split", "probit_fwd", "fwd_combine", "finalize", "bwd_coef", "bwd_elem",
            "dR_gemm", "sum_slabs", "convert", "bstat_combine", "reparam_fwd", "reparam_bwd",
-           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics", "linear", "adam"]
+           "kl_bwd", "label_weights", "fair_fwd", "fair_bwd", "metrics", "linear", "adam",
+           "adam_finish"]
 
 
 def kernel_times():

@@ -70,18 +70,22 @@ def _native_adam(opt):
     return True
 
 
-def adam_step(opt, found_inf, updates=None):
+def adam_step(opt, found_inf, updates=None, sched=None):
     """optimizer.step() of a fused torch.optim.Adam in one mpv_adam_step launch
     per parameter group (csrc/adam.hip) instead of torch's multi-tensor kernel,
     which runs the VAE's 1.5 M parameters on ~25 workgroups (DESIGN.md
-    section 11).  Same state (``step``, ``exp_avg``, ``exp_avg_sq`` in
-    ``opt.state``), same step-count protocol as torch's capturable fused path
-    (+1 before, -found_inf after), same per-element arithmetic; nothing is
-    written when ``found_inf`` is 1.  ``updates`` (an int64 device scalar, or
-    None) counts the applied updates, inside the same launch."""
+    section 11), then one mpv_adam_finish launch.  Same state (``step``,
+    ``exp_avg``, ``exp_avg_sq`` in ``opt.state``), same step-count protocol as
+    torch's capturable fused path (+1 for the update, -found_inf after), same
+    per-element arithmetic; nothing is written when ``found_inf`` is 1.
+    ``updates`` (an int64 device scalar, or None) counts the applied updates
+    and ``sched`` (a DeviceStepLR, or None) takes the scheduler step the
+    reference takes after an applied update (fairsoft_train.py:142-146), both
+    in the finish launch."""
     import mpvae_hip as H
     lib = H.load_library()
-    for g in opt.param_groups:
+    all_steps = []
+    for gi, g in enumerate(opt.param_groups):
         params = [p for p in g["params"] if p.grad is not None]
         if not params:
             continue
@@ -91,14 +95,13 @@ def adam_step(opt, found_inf, updates=None):
                 st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-        steps = [opt.state[p]["step"] for p in params]
-        torch._foreach_add_(steps, 1)
+        all_steps += [opt.state[p]["step"] for p in params]
         beta1, beta2 = g["betas"]
+        lr_dev = None if sched is None else sched.lr[gi:gi + 1]
         for c in range(0, len(params), H.ADAM_MAX_TENSORS):
             a = H.AdamArgs(n=0, lr=float(g["lr"]), beta1=float(beta1), beta2=float(beta2),
                            weight_decay=float(g["weight_decay"]), eps=float(g["eps"]),
-                           found_inf=H.ptr(found_inf), updates=H.ptr(updates))
-            updates = None  # counted once per step
+                           found_inf=H.ptr(found_inf), lr_dev=H.ptr(lr_dev))
             for p in params[c:c + H.ADAM_MAX_TENSORS]:
                 st = opt.state[p]
                 ts = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
@@ -113,8 +116,60 @@ def adam_step(opt, found_inf, updates=None):
                 a.n += 1
             H.check(lib.mpv_adam_step(ctypes.byref(a), H.stream_of(params[0].device)),
                     "mpv_adam_step")
-        if found_inf is not None:
-            torch._foreach_sub_(steps, [found_inf] * len(steps))
+    if not all_steps and updates is None and sched is None:
+        return
+    dev = (all_steps[0] if all_steps else updates if updates is not None else sched.lr).device
+    for c in range(0, max(1, len(all_steps)), H.ADAM_FINISH_MAX):
+        chunk = all_steps[c:c + H.ADAM_FINISH_MAX]
+        f = H.AdamFinishArgs(n_steps=len(chunk), found_inf=H.ptr(found_inf))
+        for i, st in enumerate(chunk):
+            f.steps[i] = st.data_ptr()
+        if c == 0:  # the counter and the scheduler step once per optimizer step
+            f.updates = H.ptr(updates)
+            if sched is not None:
+                f.n_lr, f.lr, f.last_epoch = sched.lr.numel(), H.ptr(sched.lr), \
+                    H.ptr(sched.last_epoch)
+                f.step_size, f.gamma = sched.step_size, sched.gamma
+        H.check(lib.mpv_adam_finish(ctypes.byref(f), H.stream_of(dev)), "mpv_adam_finish")
+
+
+class DeviceStepLR:
+    """The state of a torch.optim.lr_scheduler.StepLR (fairsoft_jaccard.py:67-68)
+    held on the device, so TrainStep can take the reference's scheduler step
+    (after an applied update only, fairsoft_train.py:142-145) with no host
+    sync and inside a captured graph.  ``lr`` holds one float64 learning rate
+    per param group, ``last_epoch`` the scheduler's epoch counter; both follow
+    torch's StepLR bit for bit (the chainable ``lr * gamma`` in double when
+    last_epoch is a non-zero multiple of step_size).  The optimizer's
+    ``param_groups[i]["lr"]`` and the scheduler's ``last_epoch`` /
+    ``get_last_lr()`` go stale while TrainStep owns them: ``sync()`` (one host
+    sync) writes them back, e.g. before logging or ``state_dict()``."""
+
+    def __init__(self, sched, opt):
+        if type(sched) is not torch.optim.lr_scheduler.StepLR:
+            raise ValueError("TrainStep runs torch.optim.lr_scheduler.StepLR (the reference's "
+                             f"scheduler) on the device; got {type(sched).__name__}")
+        if sched.optimizer is not opt:
+            raise ValueError("the scheduler must wrap TrainStep's optimizer")
+        dev = next(p.device for g in opt.param_groups for p in g["params"])
+        self.sched, self.opt = sched, opt
+        self.lr = torch.tensor([float(g["lr"]) for g in opt.param_groups], dtype=torch.float64,
+                               device=dev)
+        self.last_epoch = torch.tensor(int(sched.last_epoch), dtype=torch.int64, device=dev)
+        self.step_size, self.gamma = float(sched.step_size), float(sched.gamma)
+        self._epoch0 = int(sched.last_epoch)
+
+    def sync(self):
+        """Copy the device lr / last_epoch into the optimizer and the scheduler."""
+        lrs = self.lr.tolist()
+        epoch = int(self.last_epoch)
+        for g, v in zip(self.opt.param_groups, lrs):
+            g["lr"] = v
+        self.sched.last_epoch = epoch
+        self.sched._last_lr = list(lrs)
+        self.sched._step_count += epoch - self._epoch0
+        self._epoch0 = epoch
+        return lrs
 
 
 class TrainStep:
@@ -127,15 +182,17 @@ class TrainStep:
     the update on the device, step counters included -- the reference's
     ``if has_finite_grad(model): optimizer.step()`` without the host sync.
     ``updates`` counts the applied steps (the reference's succses_updates) on
-    the device.  With ``args.mpvae_noise = "philox"`` and a device-tensor
-    ``args.mpvae_seed`` nothing in the step waits for the host, so
-    ``capture()`` records it in one HIP graph (input batches are copied into
-    the static ``label`` / ``feat`` buffers before each ``replay()``).
-    A scheduler stepped only on applied updates (fairsoft_train.py:143-144)
-    needs the host, and stays the caller's (eager) business."""
+    the device.  ``scheduler``: the reference's StepLR (fairsoft_jaccard.py:
+    67-68), stepped on the device after every applied update
+    (fairsoft_train.py:142-145; DeviceStepLR, ``sync_scheduler()`` writes its
+    state back to the host objects).  With ``args.mpvae_noise = "philox"`` and
+    a device-tensor ``args.mpvae_seed`` nothing in the step waits for the
+    host, so ``capture()`` records it in one HIP graph (input batches are
+    copied into the static ``label`` / ``feat`` buffers before each
+    ``replay()``)."""
 
     def __init__(self, model, optimizer, args, max_grad_norm=10.0, advance_seed=True,
-                 native_adam=True):
+                 native_adam=True, scheduler=None):
         if not optimizer.defaults.get("fused"):
             raise ValueError("TrainStep gates the update on the device: use a fused optimizer "
                              "(torch.optim.Adam(..., fused=True))")
@@ -149,6 +206,12 @@ class TrainStep:
         self.updates = torch.zeros((), dtype=torch.int64, device=dev)
         self.found_inf = torch.zeros((), dtype=torch.float32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
+        self.sched = None
+        if scheduler is not None:
+            if not self.native_adam:
+                raise ValueError("a device StepLR needs the native Adam step (a plain fused "
+                                 "torch.optim.Adam with a float lr)")
+            self.sched = DeviceStepLR(scheduler, optimizer)
         self.graph = None
         self.label = self.feat = self.out = None
 
@@ -200,19 +263,24 @@ class TrainStep:
                 by_dtype.setdefault(p.grad.dtype, []).append(p.grad)
         for grads in by_dtype.values():
             torch._amp_foreach_non_finite_check_and_unscale_(grads, self.found_inf, self._one)
-        if self.native_adam and any(p.grad is not None for p in self.params):
-            adam_step(self.opt, self.found_inf, self.updates)
-            return res
         if self.native_adam:
-            adam_step(self.opt, self.found_inf)
+            # the update, then the step counts, `updates` and the scheduler in
+            # one finish launch (counted even when no parameter has a gradient,
+            # as the reference's gate passes such a step)
+            adam_step(self.opt, self.found_inf, self.updates, self.sched)
         else:
             self.opt.found_inf = self.found_inf
             try:
                 self.opt.step()
             finally:
                 del self.opt.found_inf
-        self.updates.add_(1 - self.found_inf.to(torch.int64))
+            self.updates.add_(1 - self.found_inf.to(torch.int64))
         return res
+
+    def sync_scheduler(self):
+        """The device StepLR's learning rates written back into the optimizer's
+        param_groups and the scheduler (one host sync); returns them."""
+        return None if self.sched is None else self.sched.sync()
 
     def __call__(self, label, feat):
         """One eager step; returns compute_loss's 8 outputs (device tensors)."""

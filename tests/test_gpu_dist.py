@@ -125,9 +125,12 @@ def test_two_ranks_on_one_gpu_match_unsharded():
         assert max(errs) <= 1e-5, (rank, errs)
 
 
-def test_bench_spawns_two_ranks_itself():
+@pytest.mark.parametrize("scaling,n_total", [("strong", 1000), ("weak", 2000)])
+def test_bench_spawns_two_ranks_itself(scaling, n_total):
     """`python bench.py --gpus 2` with no torchrun: the bench's own launcher
-    starts both ranks (gloo, both on cuda:0 here) and reports n_gpus 2."""
+    starts both ranks (gloo, both on cuda:0 here) and reports n_gpus 2.  The
+    default is strong scaling (C2's n_sample = 1000 split 500 + 500); --scaling
+    weak gives each rank its own 1000."""
     import json
     import subprocess
     import sys
@@ -136,9 +139,11 @@ def test_bench_spawns_two_ranks_itself():
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     env["MPVAE_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps",
-                        "2", "--warmup", "1", "--config", "c2", "--no-cpu-baseline"],
+                        "2", "--warmup", "1", "--config", "c2", "--no-cpu-baseline"]
+                       + ([] if scaling == "strong" else ["--scaling", "weak"]),
                        env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "n_sample-sharded x2"
-    assert line["config"]["n_sample"] == 2000 and line["loss_finite"]
+    assert line["config"]["n_sample"] == n_total and line["loss_finite"]
+    assert line["scaling"] == scaling

@@ -109,7 +109,11 @@ def test_train_metrics_training_size_against_oracle():
 def test_fair_penalty_is_graph_capturable():
     """fairness_penalty forward + backward with no host sync: captured in a HIP
     graph, replays on new batch contents equal eager calls (SURVEY 8(f) rank
-    3); a max_groups bound gives the same value as the default bound."""
+    3); a max_groups bound gives the same value as the default bound.  The
+    warm-up's autograd graph is dropped before the capture, so the leaves'
+    AccumulateGrad nodes are rebuilt on the capture stream: no stream-mismatch
+    warning (which would mean a cross-stream sync inside the graph)."""
+    import warnings
     rng = np.random.default_rng(5)
     B, L = 256, 300
     lab = torch.from_numpy((rng.random((B, L)) < 0.05).astype(np.float32)).to(DEV)
@@ -137,10 +141,15 @@ def test_fair_penalty_is_graph_capturable():
             loss.backward()
     torch.cuda.current_stream().wait_stream(side)
     a.grad = b.grad = None
+    del loss, cnt  # the warm-up's graph holds AccumulateGrad nodes made on `side`
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        loss, cnt = mf.fairness_penalty(a, b, lab, sens, tables, "l2", 0.7)
-        loss.backward()
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        with torch.cuda.graph(graph):
+            loss, cnt = mf.fairness_penalty(a, b, lab, sens, tables, "l2", 0.7)
+            loss.backward()
+    bad = [str(w.message)[:80] for w in caught if "AccumulateGrad" in str(w.message)]
+    assert not bad, bad
     for it in range(3):
         new_l = torch.from_numpy(rng.uniform(0.01, 0.99, (B, L)).astype(np.float32)).to(DEV)
         new_s = torch.from_numpy(rng.integers(0, 2 + it, (B, 2))).to(DEV)

@@ -234,9 +234,10 @@ RANDOM_CASES = [
 ]
 
 
-def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True):
+def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True, shards=1):
     """(forward errors, gradient errors) of the HIP path vs oracle.probit_elbo on
-    seeded random inputs with explicit noise."""
+    seeded random inputs with explicit noise (shards > 1: the oracle walks S in
+    that many pieces, bounding its host memory)."""
     rng = np.random.default_rng(seed)
     y = (rng.random((B, L)) < 0.25).astype(np.float32)
     y[:, 0], y[:, 1] = 1, 0
@@ -251,10 +252,11 @@ def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True)
         g_I, g_IL = np.zeros_like(g_I), np.zeros_like(g_IL)
     ref = pe.elbo_forward(inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"], inp["fx_out"],
                           inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, nll_coeff,
-                          c_coeff)
+                          c_coeff, shards=shards)
     rg = pe.elbo_backward(ref, inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"],
                           inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, nll_coeff, c_coeff,
                           g_total=1.0, g_I=g_I, g_IL=g_IL)
+    del ref
     t = {k: torch.from_numpy(v).to(DEV) for k, v in inp.items()}
     for k in DIFF + ["r_sqrt_sigma"]:
         t[k].requires_grad_(True)
@@ -310,6 +312,76 @@ def test_headline_batch_against_oracle():
     for k, e in ferr.items():
         assert e <= FWD_RTOL, (k, e)
     for k, e in gerr.items():
+        assert e <= HEADLINE_GRAD_RTOL, (k, e)
+
+
+@pytest.mark.timeout(900)
+def test_c4_dims_long_reduction_against_oracle():
+    """The C4 dR tile (dR16s_kernel<2,4,8,4>, 256 x 256) at a realistic
+    reduction length against oracle.probit_elbo itself: L = z = 1024,
+    n_sample = 4096 (the headline's), B = 32, so K = S*B = 131072 sample rows,
+    8192 per split-K chunk (16 chunks x 16 output tiles); headline
+    coefficients, total_loss as the objective.  The oracle walks S in 8 pieces
+    (about a minute of host numpy)."""
+    ferr, gerr = _against_oracle(1024, 1024, 32, 4096, 50, "f16x3", 0.1, 200.0, 4096 + 32,
+                                 with_gI=False, shards=8)
+    record("c4dims_b32_s4096_oracle", {**ferr, **{"d" + k: v for k, v in gerr.items()}})
+    for k, e in ferr.items():
+        assert e <= FWD_RTOL, (k, e)
+    for k, e in gerr.items():
+        assert e <= HEADLINE_GRAD_RTOL, (k, e)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed,gemm,with_gI", [(1, "f16x3", False), (2, "f16x3", False),
+                                               (3, "f16x3", False), (4, "f16x3", True),
+                                               (1, "f32", False)])
+def test_c4_full_size_against_fp64_reference(seed, gemm, with_gI):
+    """The headline configuration itself (BASELINE configs[3]: B = 512,
+    n_sample = 4096, L = z = 1024, nll_coeff 0.1, c_coeff 200) through
+    compute_loss fwd + bwd with explicit noise, against the oracle's formulas
+    in torch fp64 (tests/torch64_ref.py: S-chunked, on the device; pinned to
+    oracle.probit_elbo on the CPU, tests/test_torch64_ref.py).  This is the
+    size at which the dR GEMM reduces its longest split-K chunks: 2.1 M sample
+    rows, 131072 per fp32 accumulator (16 chunks x 16 tiles).  Several seeds:
+    the recorded errors are the evidence behind HEADLINE_GRAD_RTOL."""
+    from torch64_ref import ChunkedElbo
+    B, S, L, z, d = 512, 4096, 1024, 1024, 50
+    g = torch.Generator(device=DEV).manual_seed(1000 + seed)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    mus = [torch.randn((B, d), device=DEV, generator=g) * s for s in (1.0, 0.1, 1.0, 0.1)]
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * \
+        (6.0 / (L + z)) ** 0.5
+    noise = torch.randn((S, B, z), device=DEV, generator=g)
+    g_I = torch.randn((B, L), device=DEV, generator=g) if with_gI else None
+    g_IL = torch.randn((B, L), device=DEV, generator=g) if with_gI else None
+    leaves = [x.clone().requires_grad_(True) for x in (fe, mus[0], mus[1], fx, mus[2], mus[3], R)]
+    args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
+                              mode="train", nll_coeff=0.1, c_coeff=200.0, mpvae_noise=noise,
+                              mpvae_gemm=gemm)
+    out = mpvae.compute_loss(y, *leaves, args)
+    obj = out[0]
+    if with_gI:
+        obj = obj + (out[6] * g_I).sum() + (out[7] * g_IL).sum()
+    obj.backward()
+    got_out = [_np(o) for o in out]
+    got_g = {k: _np(leaves[i].grad) for k, i in (("fe_out", 0), ("fx_out", 3),
+                                                  ("r_sqrt_sigma", 6))}
+    del out, obj, leaves, args
+    torch.cuda.empty_cache()
+    ref = ChunkedElbo(y, fe, fx, R, lambda a, b: noise[a:b], S, chunk=256)
+    rf = ref.forward(*mus, 0.1, 200.0)
+    rg = ref.backward(0.1, 200.0, 1.0, g_I, g_IL)
+    errs = {k: rel_err(o, _np(rf[k])) for k, o in zip(OUTS, got_out)}
+    gerrs = {"d" + k: rel_err(v, _np(rg[k])) for k, v in got_g.items()}
+    record(f"c4_full_fp64ref_seed{seed}_{gemm}_{'with_gI' if with_gI else 'total_only'}",
+           {**errs, **gerrs})
+    for k, e in errs.items():
+        assert e <= FWD_RTOL, (k, e)
+    for k, e in gerrs.items():
         assert e <= HEADLINE_GRAD_RTOL, (k, e)
 
 

@@ -1,0 +1,59 @@
+"""CPU: the S-chunked torch fp64 restatement (tests/torch64_ref.py, used by the
+full-C4 GPU parity test) against the numpy oracle it restates
+(oracle/probit_elbo.py), which is itself pinned to the reference's golden
+vectors (tests/test_oracle_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import probit_elbo as pe
+from tolerances import rel_err
+from torch64_ref import ChunkedElbo
+
+OUTS = ["total", "nll", "nll_x", "c", "c_x", "kl", "indiv_prob", "indiv_prob_label"]
+
+
+def _case(L, z, B, S, d, seed, degenerate=False):
+    rng = np.random.default_rng(seed)
+    y = (rng.random((B, L)) < 0.25).astype(np.float32)
+    y[:, 0], y[:, 1] = 1, 0
+    if degenerate:
+        y[1] = 0.0
+        y[2] = 1.0
+    f32 = lambda a: a.astype(np.float32)
+    inp = dict(y=y, fe_out=f32(rng.standard_normal((B, L))), fx_out=f32(rng.standard_normal((B, L))),
+               fe_mu=f32(rng.standard_normal((B, d))), fe_logvar=f32(0.3 * rng.standard_normal((B, d))),
+               fx_mu=f32(rng.standard_normal((B, d))), fx_logvar=f32(0.3 * rng.standard_normal((B, d))),
+               r_sqrt_sigma=rng.uniform(-1, 1, (L, z)) * np.sqrt(6.0 / (L + z)))
+    noise = f32(rng.standard_normal((S, B, z)))
+    return inp, noise
+
+
+@pytest.mark.parametrize("L,z,B,S,chunk,degenerate", [(38, 38, 8, 40, 16, False),
+                                                      (100, 37, 5, 33, 7, False),
+                                                      (25, 10, 6, 20, 20, True)])
+@pytest.mark.parametrize("with_gI", [False, True])
+def test_chunked_torch64_matches_numpy_oracle(L, z, B, S, chunk, degenerate, with_gI):
+    inp, noise = _case(L, z, B, S, 8, L + S, degenerate)
+    rng = np.random.default_rng(1)
+    g_I = rng.standard_normal((B, L)).astype(np.float32) if with_gI else None
+    g_IL = rng.standard_normal((B, L)).astype(np.float32) if with_gI else None
+    ref = pe.elbo_forward(inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"], inp["fx_out"],
+                          inp["fx_mu"], inp["fx_logvar"], inp["r_sqrt_sigma"], noise, 0.1, 200.0)
+    rg = pe.elbo_backward(ref, inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"],
+                          inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, 0.1, 200.0,
+                          g_total=1.0, g_I=g_I, g_IL=g_IL)
+    t = {k: torch.from_numpy(v) for k, v in inp.items()}
+    nz = torch.from_numpy(noise)
+    ce = ChunkedElbo(t["y"], t["fe_out"], t["fx_out"], t["r_sqrt_sigma"], lambda a, b: nz[a:b], S,
+                     chunk)
+    out = ce.forward(t["fe_mu"], t["fe_logvar"], t["fx_mu"], t["fx_logvar"], 0.1, 200.0)
+    # torch's fp32 erf and scipy's differ by one ulp on ~1.5 % of the elements
+    # (measured: forward <= 1.1e-8, gradients <= 3.6e-8), 100x below the
+    # product's tolerances (tolerances.py)
+    for k in OUTS:
+        assert rel_err(out[k].numpy(), ref[k]) <= 5e-8, k
+    g = ce.backward(0.1, 200.0, 1.0, None if g_I is None else torch.from_numpy(g_I),
+                    None if g_IL is None else torch.from_numpy(g_IL))
+    for k in ("fe_out", "fx_out", "r_sqrt_sigma"):
+        assert rel_err(g[k].numpy(), rg[k]) <= 2e-7, k
