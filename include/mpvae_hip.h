@@ -254,6 +254,13 @@ typedef struct mpv_reparam_args {
   const float* eps_x;
   float* z_x;
   int64_t n_x;  /* elements of the feature encoder (0 = skip) */
+  /* ABI v9, each may be NULL: copies of mu / logvar written in the same pass,
+   * so the VAE hands its callers fresh tensors (not aliases of the encoder
+   * heads' outputs) at no extra launch */
+  float* mu_e_out;
+  float* logvar_e_out;
+  float* mu_x_out;
+  float* logvar_x_out;
 } mpv_reparam_args;
 
 /* Replaces label_reparameterize / feat_reparameterize (mpvae.py:66-74):

@@ -96,9 +96,13 @@ MPV_DEV void lin_load(const LinParams& p, const LinSlot& sl, int64_t row0, int64
                                : row * s_row + r * s_red;
         x = seg2 ? (IS_A ? p.a2 : p.b2)[o] : src[o];
         if (IS_A) {
-          // ReLU backward: torch's threshold_backward passes the gradient
-          // where the layer output is > 0 (NaN outputs block it)
-          if (p.a_mask != nullptr && !(p.a_mask[o] > 0.0f)) x = 0.0f;
+          // ReLU backward: torch's threshold_backward zeroes the gradient
+          // where the layer output is <= 0 (a NaN output passes it, as in
+          // torch).  With dropout folded in (the mask is the dropout output)
+          // the one difference from torch is a dropped element whose ReLU
+          // output is NaN: NaN * 0 is NaN here, so its gradient passes, where
+          // torch's dropout backward zeroes it first.
+          if (p.a_mask != nullptr && p.a_mask[o] <= 0.0f) x = 0.0f;
           x *= p.a_scale;
         }
       }

@@ -540,16 +540,21 @@ MPV_DEV void box_muller(uint32_t we, uint32_t wo, float& n0, float& n1) {
 }
 
 // Compute units of the current device (host side; 256 when it cannot be
-// queried, e.g. in a build container without a GPU).
+// queried, e.g. in a build container without a GPU).  Queried once per
+// process (a function-local static: thread-safe initialisation).  The
+// forward's s-chunk count and the dR GEMM's split-K chunk count derive from
+// it, so the order in which partial sums are added -- and with it the last
+// bits of the results -- is fixed per CU count (MI355X: 256), not across
+// devices with different CU counts.
 inline int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
+  static const int n = [] {
+    int dev = 0, v = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-  }
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    return v;
+  }();
   return n;
 }
 

@@ -20,9 +20,6 @@
 #include "abi_util.h"
 #include "mpv_common.h"
 
-#ifndef MPV_ABL
-#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
-#endif
 
 namespace mpv {
 
@@ -266,19 +263,14 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
       const int64_t cb = (int64_t)b * S + s;
       float G[4];
       f32x2 g2[4];
-      if (MPV_ABL & 16384) {  // timing study: no element math
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g2[q] = splat2(cur.t[q]) * cur.alpha + ec.base[q];
-      } else {
-        d_elem2x4(cur.t, ec, cur.alpha, cur.bP, cur.bN, g2);
-      }
+      d_elem2x4(cur.t, ec, cur.alpha, cur.bP, cur.bN, g2);
       // column sums: pad columns (finite, never published) need no mask
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         sg2[q] = sg2[q] + g2[q];
         G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
       }
-      if (PLANES && !(MPV_ABL & 32768)) {
+      if (PLANES) {
         uint16_t h[4], l[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
@@ -374,30 +366,6 @@ MPV_DEV void decode_kc_tile(int id, int K, int nT, int& kc, int& tile) {
 // Wave w moves pieces w*PER_WAVE ..; the first PIECES/2 are G rows, the rest E.
 // The global base address is the piece's first row (wave-uniform: it goes in
 // an SGPR pair); with RPP > 1 a lane's row within the piece is in its offset.
-// Timing study (MPV_ABL & 65536): the VALU a
-// dR16s producer would add if it made G from T itself, one group-0 wave's
-// share per 32-row stage: 32 rows x 256 G columns x 42.5 lane-instructions
-// (bwd_elem's measured count per label-sample) / 64 lanes / 4 waves = 1360
-// wave-instructions, as 170 x (6 fma + exp + log) on 4 independent chains.
-MPV_DEV void dr_producer_valu_study() {
-  float x0 = 1.0f, x1 = 1.1f, x2 = 1.2f, x3 = 1.3f;
-  const float c = 0.999f;
-#pragma unroll 1
-  for (int j = 0; j < 170; ++j) {
-    asm volatile(
-        "v_fma_f32 %0, %0, %4, %4\n\t"
-        "v_fma_f32 %1, %1, %4, %4\n\t"
-        "v_fma_f32 %2, %2, %4, %4\n\t"
-        "v_fma_f32 %3, %3, %4, %4\n\t"
-        "v_fma_f32 %0, %0, %4, %4\n\t"
-        "v_fma_f32 %1, %1, %4, %4\n\t"
-        "v_exp_f32 %2, %2\n\t"
-        "v_log_f32 %3, %3"
-        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
-        : "v"(c));
-  }
-}
-
 template <int PER_WAVE, int PIECES, int RPP>
 MPV_DEV void dr_issue(const Dr16Params& p, char* dst, int q0, int rows, int wid,
                       const int (&dma_off)[PER_WAVE]) {
@@ -663,7 +631,6 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
     if ((i) + 1 < nst)                                                                        \
       drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
                                   rows, wn, l0, z0, lane_u, lane_h);                          \
-    if (MPV_ABL & 65536) dr_producer_valu_study();                                            \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
     lds_barrier();                                                                            \
     __builtin_amdgcn_s_setprio(1);                                                            \

@@ -45,9 +45,6 @@ struct FwdParams {
   int nNt, nSc, tps, nSt;
 };
 
-#ifndef MPV_ABL
-#define MPV_ABL 0  // ablation bits for timing studies (tools/ablate.sh); 0 in the product
-#endif
 // Tuning constants of the product kernels (each measured; DESIGN.md section 3
 // lists the variants that lost and were removed):
 // fwd_combine: one block per batch row (512 / 256 threads: C4 0.076 -> 0.115 /
@@ -209,7 +206,7 @@ MPV_DEV void fwd_tile_epilogue(const FwdParams& p, FwdLane<TN>& ln, f32x4 (&acc)
       for (int n = 0; n < TN; ++n) {
         const bool ok = rowok && cl.colok[n];
         const float t = acc[m][n][i] * scale;
-        if (!(MPV_ABL & 2) && p.T != nullptr && ok) p.T[((int64_t)b * S + s) * p.ldT + cl.col[n]] = t;
+        if (p.T != nullptr && ok) p.T[((int64_t)b * S + s) * p.ldT + cl.col[n]] = t;
         f32x2 phi;
         const f32x2 E = probit_eval2(splat2(t) + f32x2{cl.fe[n], cl.fx[n]}, phi);
         const float y = cl.y[n];
@@ -500,7 +497,6 @@ struct Fwd16Dma {
 
   // base: wave-uniform (SGPRs); off: per-lane byte offset (inline-asm DMA, see lds_dma16)
   MPV_DEV static void piece(const char* base, uint32_t off, char* dst) {
-    if (MPV_ABL & 4) return;
     lds_dma16(base, off, lds_addr(dst));
   }
 
@@ -628,16 +624,7 @@ __global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fw
       fwd16_read<TM, TN, BM>(f, smem + (gs % NSTAGE) * STAGE, wm, wn, lr, coh, col);
       fwd16_mfma<TM, TN>(acc, f);
     }
-    if (MPV_ABL & 1) {
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int n = 0; n < TN; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
-      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
-    } else {
-      fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, st * BM, nt, red, cols);
-    }
+    fwd_tile_epilogue<WM, WN, TM, TN>(p, ln, acc, scale, b, s0, st * BM, nt, red, cols);
   }
   fwd_colsum_epilogue<WM, WN, TM, TN>(p, ln, b, sc, n0, red);
 }
@@ -779,7 +766,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       __builtin_amdgcn_s_setprio(1);
     else
       __builtin_amdgcn_s_setprio(0);
-    if (!(MPV_ABL & 2) && p.T != nullptr) {
+    if (p.T != nullptr) {
       // T stash of this label group, at the top of its iteration (all 16
       // stores up front kept the prio-0 waves 4-8 K cycles in store issue)
 #pragma unroll
@@ -1023,7 +1010,7 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
 #pragma unroll
       for (int n = 0; n < TS; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
       if (NSTAGE == 2)
         wait_vmcnt<0>();
       else
@@ -1035,49 +1022,16 @@ __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kern
       fwd16t_read<WL, TL, TS, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, ws * TS, lr, coh, col);
       fwd16t_mfma<TL, TS>(acc, f);
     }
-    if (MPV_ABL & 1) {  // timing study: no epilogue
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TS; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
-      p.rowpart[(int64_t)blockIdx.x * 256 + tid] = v;
-    } else {
+    __builtin_amdgcn_s_setprio(0);
+    fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
+                                        soft_any);
+    // back to the K-loop priorities
+    if (wid >= NW / 2)
+      __builtin_amdgcn_s_setprio(1);
+    else
       __builtin_amdgcn_s_setprio(0);
-      fwd_tile_epilogue_t<WL, WS, TL, TS>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
-                                          soft_any);
-      // back to the K-loop priorities
-      if (wid >= NW / 2)
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
-    }
   }
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
-}
-
-// Timing study (MPV_ABL & 65536): the VALU an
-// in-kernel noise generator would add to the forward, one DMA wave's share
-// per 32-K stage: 128 samples x 32 normals x 26.8 lane-instructions
-// (noise_philox16's measured count per normal) / 64 lanes / 4 waves = 429
-// wave-instructions, as 54 x (6 fma + exp + log) on 4 register chains.
-MPV_DEV void fwd_noise_valu_study() {
-  float x0 = 1.0f, x1 = 1.1f, x2 = 1.2f, x3 = 1.3f;
-  const float c = 0.999f;
-#pragma unroll 1
-  for (int j = 0; j < 54; ++j) {
-    asm volatile(
-        "v_fma_f32 %0, %0, %4, %4\n\t"
-        "v_fma_f32 %1, %1, %4, %4\n\t"
-        "v_fma_f32 %2, %2, %4, %4\n\t"
-        "v_fma_f32 %3, %3, %4, %4\n\t"
-        "v_fma_f32 %0, %0, %4, %4\n\t"
-        "v_fma_f32 %1, %1, %4, %4\n\t"
-        "v_exp_f32 %2, %2\n\t"
-        "v_log_f32 %3, %3"
-        : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3)
-        : "v"(c));
-  }
 }
 
 // ------------------------- 3xf16, asymmetric sample split (probit_fwd16a)
@@ -1105,27 +1059,17 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
     for (int m = 0; m < TL; ++m)
 #pragma unroll
       for (int n = 0; n < TSW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kc = 0; kc < ((MPV_ABL & 8) ? 0 : nK); ++kc, ++gs) {
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
       wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
       if (dmaw) {
         dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
                   t_end, nK, b);
-        if (MPV_ABL & 65536) fwd_noise_valu_study();
       }
       FragT<TL, TSW> f;
       fwd16t_read<WL, TL, TSW, BM>(f, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
       fwd16t_mfma<TL, TSW>(acc, f);
-    }
-    if (MPV_ABL & 1) {  // timing study: no epilogue
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < TL; ++m)
-#pragma unroll
-        for (int n = 0; n < TSW; ++n) v += acc[m][n][0] + acc[m][n][1] + acc[m][n][2] + acc[m][n][3];
-      p.rowpart[(int64_t)blockIdx.x * 512 + threadIdx.x] = v;
-      continue;
     }
     __builtin_amdgcn_s_setprio(0);
     fwd_tile_epilogue_t<WL, 2, TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc, cols,
@@ -1135,7 +1079,6 @@ MPV_DEV void fwd16a_tiles(const FwdParams& p, char* smem, float* red, float* cac
     else
       __builtin_amdgcn_s_setprio(0);
   }
-  if (MPV_ABL & 8) wait_vmcnt<0>();  // timing study: no stage DMA left in flight at exit
 }
 
 template <int TSA, int TSB, int TL>

@@ -258,10 +258,16 @@ __global__ void bstat_combine_kernel(const float* __restrict__ g, int64_t R, int
 __global__ void reparam_fwd_kernel(mpv_reparam_args a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < a.n_e) {
-    a.z_e[i] = a.mu_e[i] + a.eps_e[i] * expf(0.5f * a.logvar_e[i]);
+    const float mu = a.mu_e[i], lv = a.logvar_e[i];
+    a.z_e[i] = mu + a.eps_e[i] * expf(0.5f * lv);
+    if (a.mu_e_out != nullptr) a.mu_e_out[i] = mu;
+    if (a.logvar_e_out != nullptr) a.logvar_e_out[i] = lv;
   } else if (i - a.n_e < a.n_x) {
     const int64_t j = i - a.n_e;
-    a.z_x[j] = a.mu_x[j] + a.eps_x[j] * expf(0.5f * a.logvar_x[j]);
+    const float mu = a.mu_x[j], lv = a.logvar_x[j];
+    a.z_x[j] = mu + a.eps_x[j] * expf(0.5f * lv);
+    if (a.mu_x_out != nullptr) a.mu_x_out[j] = mu;
+    if (a.logvar_x_out != nullptr) a.logvar_x_out[j] = lv;
   }
 }
 

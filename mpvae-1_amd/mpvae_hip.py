@@ -73,7 +73,8 @@ class KlBwdArgs(ctypes.Structure):
 
 class ReparamArgs(ctypes.Structure):
     _fields_ = [("mu_e", vp), ("logvar_e", vp), ("eps_e", vp), ("z_e", vp), ("n_e", ctypes.c_int64),
-                ("mu_x", vp), ("logvar_x", vp), ("eps_x", vp), ("z_x", vp), ("n_x", ctypes.c_int64)]
+                ("mu_x", vp), ("logvar_x", vp), ("eps_x", vp), ("z_x", vp), ("n_x", ctypes.c_int64),
+                ("mu_e_out", vp), ("logvar_e_out", vp), ("mu_x_out", vp), ("logvar_x_out", vp)]
 
 
 class ReparamBwdArgs(ctypes.Structure):

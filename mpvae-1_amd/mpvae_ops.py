@@ -366,11 +366,12 @@ class FusedReparam(torch.autograd.Function):
     launch (mpvae.py:66-74).  eps is an input (drawn by the caller with
     torch.randn_like, so the RNG stream matches the reference's draw order).
 
-    mu and logvar are also passed through as outputs: the VAE returns those
-    (same tensors' values) to the caller, so the gradient compute_loss's KL
-    sends them arrives here and is added inside mpv_reparam_bwd -- the one
-    add autograd would otherwise launch per tensor when two consumers of an
-    encoder head meet."""
+    mu and logvar are also returned, as fresh copies the kernel writes in the
+    same pass (ordinary tensors: a caller may modify them in place, as it may
+    the reference's): the VAE returns those to the caller, so the gradient
+    compute_loss's KL sends them arrives here and is added inside
+    mpv_reparam_bwd -- the one add autograd would otherwise launch per tensor
+    when two consumers of an encoder head meet."""
 
     @staticmethod
     def forward(ctx, mu_e, lv_e, eps_e, mu_x, lv_x, eps_x):
@@ -378,12 +379,14 @@ class FusedReparam(torch.autograd.Function):
         mu_e, lv_e, eps_e = (_f32(t, "reparam input") for t in (mu_e, lv_e, eps_e))
         mu_x, lv_x, eps_x = (_f32(t, "reparam input") for t in (mu_x, lv_x, eps_x))
         z_e, z_x = torch.empty_like(mu_e), torch.empty_like(mu_x)
+        outs = [torch.empty_like(t) for t in (mu_e, lv_e, mu_x, lv_x)]
         a = H.ReparamArgs(H.ptr(mu_e), H.ptr(lv_e), H.ptr(eps_e), H.ptr(z_e), mu_e.numel(),
-                          H.ptr(mu_x), H.ptr(lv_x), H.ptr(eps_x), H.ptr(z_x), mu_x.numel())
+                          H.ptr(mu_x), H.ptr(lv_x), H.ptr(eps_x), H.ptr(z_x), mu_x.numel(),
+                          *[H.ptr(o) for o in outs])
         H.check(H.load_library().mpv_reparam_fwd(a, H.stream_of(mu_e.device)), "mpv_reparam_fwd")
         ctx.save_for_backward(lv_e, eps_e, lv_x, eps_x)
         ctx.set_materialize_grads(False)
-        return z_e, z_x, mu_e, lv_e, mu_x, lv_x
+        return (z_e, z_x, *outs)
 
     @staticmethod
     def backward(ctx, gz_e, gz_x, gmu_e_in, glv_e_in, gmu_x_in, glv_x_in):
@@ -411,7 +414,7 @@ class SingleReparam(torch.autograd.Function):
         mu, lv, eps = (_f32(t, "reparam input") for t in (mu, lv, eps))
         z = torch.empty_like(mu)
         a = H.ReparamArgs(H.ptr(mu), H.ptr(lv), H.ptr(eps), H.ptr(z), mu.numel(),
-                          None, None, None, None, 0)
+                          None, None, None, None, 0, None, None, None, None)
         H.check(H.load_library().mpv_reparam_fwd(a, H.stream_of(mu.device)), "mpv_reparam_fwd")
         ctx.save_for_backward(lv, eps)
         return z

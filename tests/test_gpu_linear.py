@@ -110,8 +110,9 @@ def test_linear_graph_capture():
 
 
 def test_linear_nan_and_relu_semantics():
-    """torch.relu passes NaN; the ReLU backward blocks the gradient where the
-    output is 0 or NaN (threshold_backward)."""
+    """torch.relu passes NaN; its backward (threshold_backward) zeroes the
+    gradient only where the output is <= 0, so a NaN output passes it: the
+    kernel's ReLU mask does the same."""
     layer = _layer(8, 4)
     x = torch.randn((3, 8), device=DEV)
     x[1, 2] = float("nan")
@@ -121,8 +122,13 @@ def test_linear_nan_and_relu_semantics():
     assert torch.equal(torch.isnan(y), torch.isnan(y_t))
     assert torch.isnan(y[1]).all()
     y.backward(torch.ones_like(y))
-    # row 1's output is NaN everywhere, so no gradient flows back through it
-    assert torch.equal(x.grad[1], torch.zeros_like(x.grad[1]))
+    xt = x.detach().clone().requires_grad_(True)
+    lt = _layer(8, 4)
+    torch.relu(torch.nn.functional.linear(xt, lt.weight, lt.bias)).backward(torch.ones_like(y))
+    # row 1's output is NaN everywhere and torch passes the gradient through it
+    assert torch.isfinite(x.grad[1]).all() and x.grad[1].abs().max() > 0
+    torch.testing.assert_close(x.grad, xt.grad, rtol=2e-6, atol=1e-6)
+    assert torch.equal(torch.isnan(layer.weight.grad), torch.isnan(lt.weight.grad))
     assert torch.isnan(layer.weight.grad).any()  # x's NaN reaches dW (as in torch)
 
 

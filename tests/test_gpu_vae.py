@@ -413,3 +413,12 @@ def test_fused_reparam_passthrough_grads_bit_equal():
         return torch.autograd.grad(loss, leaves)
     for a, b in zip(grads(True), grads(False)):
         assert torch.equal(a, b)
+    # the returned mu / logvar are fresh tensors, not views of the heads: a
+    # caller may modify them in place, as it may the reference's
+    h = [t * 1.0 for t in leaves]
+    out = FusedReparam.apply(h[0], h[1], eps_e, h[2], h[3], eps_x)
+    assert all(o._base is None and o.data_ptr() != x.data_ptr() for o, x in zip(out[2:], h))
+    assert all(torch.equal(o, x) for o, x in zip(out[2:], h))
+    out[2].clamp_(-1.0, 1.0)
+    (out[2].sum() + out[0].sum()).backward()
+    assert torch.isfinite(leaves[0].grad).all()

@@ -17,6 +17,8 @@ y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
 y[:, 0], y[:, 1] = 1, 0
 fe = torch.randn((B, L), device=DEV, generator=g)
 fx = torch.randn((B, L), device=DEV, generator=g)
+if os.environ.get("PROBE_SWAP") == "1":  # the two branches' means exchanged
+    fe, fx = fx, fe
 R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.03
 be = HipShardBackend()
 shape = be.shape(S, S, 0, B, L, z)
@@ -38,12 +40,25 @@ def one(keep):
 
 first, gfirst = one(True)
 bad_runs, bad_k, bad_g = 0, set(), 0
+detail = os.environ.get("PROBE_DETAIL") == "1"
+shown = 0
 for _ in range(runs):
     rs, gr = one(keep_T)
     d = rs != first
     if d.any():
         bad_runs += 1
         bad_k |= set(torch.nonzero(d)[:, 0].tolist())
+        if detail and shown < 4:
+            # which (stat, b, s) differ, by how much, and in how many
+            # (b, 16-sample block) groups; the first launch as the reference
+            shown += 1
+            idx = torch.nonzero(d)
+            blocks = sorted({(int(b), int(s) // 16) for _, b, s in idx.tolist()})
+            print(f"  run differs in {idx.shape[0]} entries, {len(blocks)} (b, s//16) blocks "
+                  f"{blocks[:6]}", flush=True)
+            for k, b, s_ in idx[:6].tolist():
+                a, c = float(first[k, b, s_]), float(rs[k, b, s_])
+                print(f"    k={k} b={b} s={s_}: {a:.9g} -> {c:.9g} (diff {c - a:.6g})", flush=True)
     if bwd and not torch.equal(gr, gfirst):
         bad_g += 1
 torch.cuda.synchronize()
