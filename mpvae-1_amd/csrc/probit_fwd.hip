@@ -879,10 +879,12 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // The row sums sp / sn were last written inside pk_fma2_acc_bc's asm, which
   // hipcc's hazard recognizer cannot see into; a VALU write must be 2 wait
   // states ahead of the v_permlane*_swap that reads it (sum_lanegroups_n).
-  // Without this pad the swap could read the value before the last label's
-  // update, depending on how the SIMD's other wave interleaved: rowstat N
-  // was off by one e^{5E} term for 16-sample rows, run to run (found by
-  // tests/test_gpu_parity.py's full-size determinism test at C3).
+  // (The pad is required by the ISA.  It is NOT what made the round-3
+  // 4-wave, two-workgroups-per-CU tile repeatable: that tile still loses one
+  // label-branch update of one 16-lane row with the pad in place, with no
+  // inline asm at all, with ds_bpermute sums instead of permlanes, and without
+  // the T stash; only one workgroup per CU removes it.  DESIGN.md section 3,
+  // "the round-3 lost update", tools/race_study.sh.)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 1" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);

@@ -21,6 +21,7 @@ paths are reported separately with the label noted).
 import re
 import sys
 
+ALL = False
 TRANS = re.compile(r"^v_(exp|log|rcp|rsq|sqrt|sin|cos)_f(16|32)")
 REG = re.compile(r"\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]")
 
@@ -108,7 +109,7 @@ def scan(ins):
                     continue
                 hit = pd & reads
                 if hit:
-                    if is_prod(pm, pd) and waits < need and (asm_i or asm_j):
+                    if is_prod(pm, pd) and waits < need and (asm_i or asm_j or ALL):
                         found.append((name, waits, need, ins[i][4], raw, crossed))
                     reads = reads - hit
                     if not reads:

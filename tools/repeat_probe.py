@@ -30,6 +30,8 @@ bwd = os.environ.get("PROBE_BWD") == "1"
 
 def one(keep):
     loc = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep or bwd)
+    if os.environ.get("PROBE_T") == "1" and keep:  # compare the T stash too
+        return loc["rowstat"].clone(), loc["T"].clone()
     if not bwd:
         return loc["rowstat"].clone(), None
     saved = dict(y=y, fe_out=fe, fx_out=fx, eps=eps, T=loc["T"], rowstat=loc["rowstat"],
@@ -59,9 +61,13 @@ for _ in range(runs):
             for k, b, s_ in idx[:6].tolist():
                 a, c = float(first[k, b, s_]), float(rs[k, b, s_])
                 print(f"    k={k} b={b} s={s_}: {a:.9g} -> {c:.9g} (diff {c - a:.6g})", flush=True)
-    if bwd and not torch.equal(gr, gfirst):
+    if (bwd or gr is not None) and not torch.equal(gr, gfirst):
         bad_g += 1
+        if detail and not bwd:
+            dt = torch.nonzero(gr != gfirst)
+            print(f"  T differs in {dt.shape[0]} elements, first {dt[:4].tolist()}", flush=True)
 torch.cuda.synchronize()
 print(f"{os.environ.get('MPVAE_HIP_LIB', 'x/default/x').split('/')[-2]} B={B} S={S} L={L}: "
       f"keep_T={keep_T} {bad_runs}/{runs} runs differ, stats {sorted(bad_k)}"
-      + (f"; backward: {bad_g}/{runs} differ" if bwd else ""), flush=True)
+      + (f"; backward/T: {bad_g}/{runs} differ" if (bwd or gfirst is not None) else ""),
+      flush=True)
