@@ -256,7 +256,6 @@ def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True,
     rg = pe.elbo_backward(ref, inp["y"], inp["fe_out"], inp["fe_mu"], inp["fe_logvar"],
                           inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, nll_coeff, c_coeff,
                           g_total=1.0, g_I=g_I, g_IL=g_IL)
-    del ref
     t = {k: torch.from_numpy(v).to(DEV) for k, v in inp.items()}
     for k in DIFF + ["r_sqrt_sigma"]:
         t[k].requires_grad_(True)
