@@ -43,8 +43,14 @@ def probit_prob(u32):
     return (cdf.astype(F32) * C1 + C0).astype(F32)
 
 
-def noise_product(noise, R):
-    """t = tensordot(noise, R.T.float()) -> (S,B,L) float32 (mpvae.py:165-170)."""
+def noise_product(noise, R, t_fp32=False):
+    """t = tensordot(noise, R.T.float()) -> (S,B,L) float32 (mpvae.py:165-170),
+    accumulated in fp64 and rounded once; t_fp32: by an fp32 GEMM, as the
+    reference's own tensordot computes it (to measure how far fp32 arithmetic
+    alone moves the results)."""
+    if t_fp32:
+        Rt32 = np.asarray(R).astype(F32).T
+        return np.asarray(noise, F32) @ Rt32
     Rt = np.asarray(R).astype(F32).astype(np.float64).T          # (z, L)
     t = np.asarray(noise, np.float64) @ Rt
     return t.astype(F32)
@@ -85,7 +91,7 @@ def branch_rows(E, y, ranking="factorized"):
     return logp, P, N, c
 
 
-def shard_forward(y, fe_out, fx_out, R, noise, ranking="factorized"):
+def shard_forward(y, fe_out, fx_out, R, noise, ranking="factorized", t_fp32=False):
     """Statistics of one S-shard (noise = this shard's (S_loc,B,z) slice).
 
     Returns dict with
@@ -94,7 +100,7 @@ def shard_forward(y, fe_out, fx_out, R, noise, ranking="factorized"):
       colsum  (2,B,L)     = [sum_s E, sum_s E_x]
       E, Ex, t            (S_loc,B,L) for the backward
     """
-    t = noise_product(noise, R)
+    t = noise_product(noise, R, t_fp32)
     E = probit_prob(t + np.asarray(fe_out, F32))
     Ex = probit_prob(t + np.asarray(fx_out, F32))
     le, Pe, Ne, ce = branch_rows(E, y, ranking)
@@ -225,11 +231,12 @@ def kl_backward(mu_e, lv_e, mu_x, lv_x, g_kl):
 
 # ---------------------------------------------------------------- one-shot API
 def elbo_forward(y, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar, R, noise,
-                 nll_coeff, c_coeff, ranking="factorized", shards=1):
-    """Whole compute_loss forward; ``shards`` > 1 splits S and combines exactly."""
+                 nll_coeff, c_coeff, ranking="factorized", shards=1, t_fp32=False):
+    """Whole compute_loss forward; ``shards`` > 1 splits S and combines exactly;
+    ``t_fp32``: t from an fp32 GEMM (noise_product)."""
     S = noise.shape[0]
     edges = np.linspace(0, S, shards + 1).astype(int)
-    parts = [shard_forward(y, fe_out, fx_out, R, noise[a:b], ranking)
+    parts = [shard_forward(y, fe_out, fx_out, R, noise[a:b], ranking, t_fp32)
              for a, b in zip(edges[:-1], edges[1:])]
     bstat = combine_bstats([p["bstat"] for p in parts])
     colsum = sum(p["colsum"] for p in parts)
