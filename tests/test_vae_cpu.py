@@ -131,3 +131,36 @@ def test_train_step_clip_matches_torch(scale):
             assert torch.equal(p1.grad, p2.grad), k
         else:
             torch.testing.assert_close(p1.grad, p2.grad, rtol=2 ** -23, atol=0, msg=k)
+
+
+def test_device_steplr_contract():
+    """Host-side contract of TrainStep's device StepLR (mpvae_step.DeviceStepLR):
+    only the reference's torch.optim.lr_scheduler.StepLR, wrapping TrainStep's
+    own optimizer, on the native Adam path; the device state starts from the
+    scheduler's and sync() writes it back (fairsoft_jaccard.py:64-68)."""
+    import mpvae_step
+    args = argparse.Namespace(feature_dim=6, latent_dim=4, label_dim=5, z_dim=3, keep_prob=0.5,
+                              scale_coeff=1.0, residue_sigma="", mpvae_linear="torch")
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = mpvae.VAE(args)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    other = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 37.5, 0.5)
+    with pytest.raises(ValueError, match="StepLR"):
+        mpvae_step.DeviceStepLR(torch.optim.lr_scheduler.ExponentialLR(opt, 0.9), opt)
+    with pytest.raises(ValueError, match="wrap"):
+        mpvae_step.DeviceStepLR(torch.optim.lr_scheduler.StepLR(other, 2), opt)
+    # CPU parameters: not the native (device) Adam path, so no device scheduler
+    with pytest.raises(ValueError, match="native Adam"):
+        mpvae_step.TrainStep(model, opt, args, scheduler=sched)
+    d = mpvae_step.DeviceStepLR(sched, opt)
+    assert d.lr.dtype == torch.float64 and d.lr.tolist() == [1e-3]
+    assert int(d.last_epoch) == sched.last_epoch == 0
+    assert d.step_size == 37.5 and d.gamma == 0.5
+    # a device step that decayed (as mpv_adam_finish does at a multiple of step_size)
+    d.last_epoch.fill_(75)
+    d.lr.mul_(0.5)
+    assert d.sync() == [5e-4]
+    assert opt.param_groups[0]["lr"] == 5e-4 and sched.last_epoch == 75
+    assert sched.get_last_lr() == [5e-4]
