@@ -16,7 +16,7 @@ checked at the looser level.
 """
 
 # Each tolerance sits at 1-5x the largest error measured on the MI355X for the
-# cases it covers (profiles/r03_parity_errors.json, recorded by these tests
+# cases it covers (profiles/r04_parity_errors.json, recorded by these tests
 # with MPVAE_RECORD_ERRS set); the comment gives that measurement.
 FWD_RTOL = 2e-6    # measured <= 4.8e-7 (golden, random, C2/C3 full size, eval 10000)
 GRAD_RTOL = 5e-5   # measured <= 4.1e-5 (random cases with K ~ 1000 noise dims; golden <= 6.3e-6)
@@ -105,7 +105,7 @@ def params_track(test_id, p1, p2, lr, steps, losses=None):
 def record(test_id, errs):
     """Append the measured errors of one parity case to
     $MPVAE_RECORD_ERRS (a JSON-lines file) when that is set: the evidence
-    behind the tolerances above (profiles/r03_parity_errors.json)."""
+    behind the tolerances above (profiles/r04_parity_errors.json)."""
     import json
     import os
     path = os.environ.get("MPVAE_RECORD_ERRS")
