@@ -267,7 +267,7 @@ def _against_oracle(L, z, B, S, d, gemm, nll_coeff, c_coeff, seed, with_gI=True,
                                 inp["fx_out"], inp["fx_mu"], inp["fx_logvar"], noise, nll_coeff,
                                 c_coeff, g_total=1.0, g_I=g_I, g_IL=g_IL)
         del r32
-        spread.update({"ref_fp32_d" + k: rel_err(rg32[k], rg[k])
+        spread.update({"d" + k + "_ref_fp32": rel_err(rg32[k], rg[k])
                        for k in ("fe_out", "fx_out", "r_sqrt_sigma")})
     t = {k: torch.from_numpy(v).to(DEV) for k, v in inp.items()}
     for k in DIFF + ["r_sqrt_sigma"]:
@@ -410,7 +410,7 @@ def test_c4_full_size_against_fp64_reference(seed, gemm, with_gI):
     del ref32
     errs = {k: rel_err(o, _np(rf[k])) for k, o in zip(OUTS, got_out)}
     gerrs = {"d" + k: rel_err(v, _np(rg[k])) for k, v in got_g.items()}
-    spread = {"ref_fp32_d" + k: rel_err(_np(rg32[k]), _np(rg[k])) for k in got_g}
+    spread = {"d" + k + "_ref_fp32": rel_err(_np(rg32[k]), _np(rg[k])) for k in got_g}
     record(f"c4_full_fp64ref_seed{seed}_{gemm}_{'with_gI' if with_gI else 'total_only'}",
            {**errs, **gerrs, **spread})
     for k, e in errs.items():

@@ -18,7 +18,7 @@ checked at the looser level.
 # Each tolerance sits at 1-5x the largest error measured on the MI355X for the
 # cases it covers (profiles/r04_parity_errors.json, recorded by these tests
 # with MPVAE_RECORD_ERRS set); the comment gives that measurement.
-FWD_RTOL = 2e-6    # measured <= 4.8e-7 (golden, random, C2/C3 full size, eval 10000)
+FWD_RTOL = 2e-6    # measured <= 8.9e-7 (golden, random, C2/C3/C4 full size, eval 10000; r04)
 GRAD_RTOL = 5e-5   # measured <= 4.1e-5 (random cases with K ~ 1000 noise dims; golden <= 6.3e-6)
 # Long noise GEMMs (z = 4096): the gradient w.r.t. fe_out / fx_out / R is
 # conditioned at the 1e-4 level by the fp32 rounding of t = eps . R^T alone:
