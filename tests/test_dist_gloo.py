@@ -1,4 +1,4 @@
-"""Multi-rank S-sharding on CPU (gloo, world_size 2 and 3): the product's
+"""Multi-rank S-sharding on CPU (gloo, world_size 2, 3 and 8): the product's
 autograd Function + cross-rank exchange (mpvae_dist) with an oracle shard
 backend must reproduce the unsharded golden values and gradients."""
 import os
@@ -54,8 +54,10 @@ def _worker(rank, world, port, names, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_elbo_matches_unsharded_reference(world):
+    """world 8 rehearses the driver's 8-GPU node on the CPU (ragged shards:
+    16 samples as 2 each, 12 as 2,2,2,2,1,1,1,1)."""
     names = ["f1_l38", "f2_degenerate", "f3_adult_like"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
