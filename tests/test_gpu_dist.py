@@ -74,7 +74,7 @@ def test_rccl_exchange_world_one_matches_local():
 
 
 def _gloo_worker(rank, world, port, q):
-    """One rank of a 2-rank job sharing cuda:0, exchange over gloo on device
+    """One rank of an N-rank job sharing cuda:0, exchange over gloo on device
     tensors: the HIP shard backend + SampleShardExchange + a real N-rank
     all_gather of bstat, against the unsharded call on the same inputs."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -82,7 +82,7 @@ def _gloo_worker(rank, world, port, q):
     try:
         torch.cuda.set_device(0)
         g = torch.Generator(device=DEV).manual_seed(11)
-        B, L, z, d, S = 64, 100, 90, 8, 777           # ragged: 389 + 388 samples
+        B, L, z, d, S = 64, 100, 90, 8, 777           # ragged: 389 + 388, or 98 x 1 + 97 x 7
         y = (torch.rand((B, L), device=DEV, generator=g) < 0.2).float()
         y[:, 0], y[:, 1] = 1, 0
         mk = lambda *s: torch.randn(*s, device=DEV, generator=g)
@@ -109,18 +109,23 @@ def _gloo_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_unsharded():
+@pytest.mark.parametrize("world", [2, 8])
+def test_ranks_on_one_gpu_match_unsharded(world):
+    """2 ranks, and the driver's 8 (each with its own HIP context on cuda:0;
+    an RCCL group cannot hold two ranks of one device, so gloo carries the
+    collectives): loss, indiv_prob and gradients equal the unsharded call."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=100) for _ in procs]
+    res = [q.get(timeout=150) for _ in procs]
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
+    assert sorted(r for r, _ in res) == list(range(world))
     for rank, errs in res:
         assert max(errs) <= 1e-5, (rank, errs)
 
