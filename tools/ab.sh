@@ -19,7 +19,7 @@ for rep in ${REPS:-1 2}; do
     for c in $CFGS; do
       g=--graph; [ "$c" = c4 ] || [ "$c" = c5 ] && g=
       MPVAE_HIP_LIB=$(lib_of $v) step ${c}_${v}_$rep 300 python bench.py --config $c $g \
-        --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline
+        --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline $BENCH_EXTRA
       python -c "import json;d=json.load(open('$O/${c}_${v}_$rep.out'));print('$c $v',round(d['ms_per_step'],4),d['roofline']['ms_per_step_by_op'])"
     done
   done
