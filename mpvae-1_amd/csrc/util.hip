@@ -100,18 +100,20 @@ __global__ void noise_philox_kernel(float* __restrict__ eps, int64_t e_begin, in
                                     const uint64_t* __restrict__ seed_dev) {
   philox_key(seed_dev, k0, k1);
   const int64_t g0 = e_begin >> 2;  // first counter touching the shard
-  const int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t e_end = e_begin + e_count;
-  if ((g << 2) >= e_end) return;
-  const uint64_t ctr = (uint64_t)g + offset;
-  const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
-  float n[4];
-  box_muller(w.x, w.y, n[0], n[1]);
-  box_muller(w.z, w.w, n[2], n[3]);
+  // grid-stride: a launch is capped below 2^32 threads, a C5 shard is not
+  for (int64_t g = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; (g << 2) < e_end;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t ctr = (uint64_t)g + offset;
+    const u32x4 w = philox4x32_10(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u}, k0, k1);
+    float n[4];
+    box_muller(w.x, w.y, n[0], n[1]);
+    box_muller(w.z, w.w, n[2], n[3]);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t e = (g << 2) + q;
-    if (e >= e_begin && e < e_end) eps[e - e_begin] = n[q];
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = (g << 2) + q;
+      if (e >= e_begin && e < e_end) eps[e - e_begin] = n[q];
+    }
   }
 }
 
@@ -557,8 +559,7 @@ static int noise_philox(float* eps, const mpv_shape* shape, uint64_t seed,
   const int64_t first = e_begin >> 2, last = (e_begin + e_count - 1) >> 2;
   const int64_t nthreads = last - first + 1;
   const int threads = 256;
-  const int64_t blocks = cdiv(nthreads, threads);
-  MPV_REQUIRE(blocks < (int64_t(1) << 31), "noise too large");
+  const int64_t blocks = std::min<int64_t>(cdiv(nthreads, threads), int64_t(1) << 22);
   MPV_LAUNCH("noise_philox", noise_philox_kernel, dim3((unsigned)blocks), dim3(threads), 0,
                      as_stream(stream), eps, e_begin, e_count, (uint32_t)seed,
                      (uint32_t)(seed >> 32), offset, seed_dev);

@@ -56,6 +56,19 @@ HEADLINE_GRAD_RTOL = 5e-4
 # measure <= 8.8e-4 (seed 78, d fx_out).  The tests assert the reference's
 # own spread under the same bound.
 C4_FULL_GRAD_RTOL = 1.5e-3
+# BASELINE configs[4] at full size on one GPU (B = 512, n_sample = 8192,
+# L = z = 4096), philox noise, total_loss, against the S-chunked fp64-t
+# restatement.  Four times the labels per sample: more elements one ulp from
+# E = 1, and the same per-element effect.  Measured over seeds 11-14
+# (profiles/r04_c5_fp64ref.json): the reference's own fp32 arithmetic lands
+# <= 2.6e-3 from the fp64-t values, the same formulas with a correctly rounded
+# fp32 erf <= 1.5e-3, the f16x3 kernels <= 1.6e-3 on three seeds and 3.6e-3
+# on one (seed 11, d fe_out; there the exact-fp32 MFMA mode gives 1.06e-3 and
+# the fp32 reference 1.04e-3: a different set of one-ulp roundings, not a
+# bias -- tools/t_accuracy.py finds the 3xf16 t closer to the fp64 product
+# than an fp32 GEMM's, mean |err| 5.0e-7 against 8.0e-7 at K = 4096).  The
+# tests assert the reference's own spread under the same bound.
+C5_FULL_GRAD_RTOL = 5e-3
 # The extreme-logit fixture (|u| up to ~20): E near the 0.5e-6 floor, where
 # torch-CPU's and scipy's erf disagree by up to 1.3e-2 in the gradient
 # (module docstring).  Measured: forward 3.6e-5, gradients 1.3e-2.

@@ -28,11 +28,16 @@ INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
 KL_EPS, KL_WEIGHT = 1e-6, 1.1
 
 
-def probit_prob(u32):
-    """E = Normal(0,1).cdf(u)(1-eps1) + eps1/2 in float32, op by op (oracle.probit_prob)."""
+def probit_prob(u32, erf_fp64=False):
+    """E = Normal(0,1).cdf(u)(1-eps1) + eps1/2 in float32, op by op (oracle.probit_prob).
+    erf_fp64: erf(x) evaluated in float64 and rounded once to float32 (a
+    correctly rounded fp32 erf) in place of torch's fp32 erf -- the same
+    formula with another legitimate fp32 erf, to measure what one-ulp
+    differences of E alone do to the gradients."""
     d = u32.device
     x = u32 / _SQRT2.to(d)
-    cdf = 0.5 * (1.0 + torch.erf(x))
+    erf = torch.erf(x.to(F64)).to(F32) if erf_fp64 else torch.erf(x)
+    cdf = 0.5 * (1.0 + erf)
     return cdf * _C1.to(d) + _C0.to(d)
 
 
@@ -48,7 +53,7 @@ class ChunkedElbo:
     samples [s0, s1) on the inputs' device (it is called twice per chunk:
     forward and backward, and must return the same values)."""
 
-    def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False):
+    def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False, erf_fp64=False):
         self.y, self.fe, self.fx = y.to(F32), fe_out.to(F32), fx_out.to(F32)
         self.Rt = R.to(F32).to(F64).t().contiguous()          # R.T.float() (mpvae.py:165)
         self.noise, self.S, self.chunk = noise, int(S), int(chunk)
@@ -56,6 +61,7 @@ class ChunkedElbo:
         # it (mpvae.py:168-170), instead of fp64 accumulation rounded once --
         # measures how far fp32 arithmetic alone moves the results
         self.t_fp32 = bool(t_fp32)
+        self.erf_fp64 = bool(erf_fp64)
         self.pos, self.neg, self.n = label_sets(self.y)
         self.y64 = self.y.to(F64)
 
@@ -89,7 +95,7 @@ class ChunkedElbo:
         for s0, s1 in self._chunks():
             t, _ = self._t(s0, s1)
             for br, base in enumerate((self.fe, self.fx)):
-                E = probit_prob(t + base)
+                E = probit_prob(t + base, self.erf_fp64)
                 logp, P, N, c = self._rows(E)
                 rows[br, :, s0:s1] = logp.t()
                 rows[2 + 2 * br, :, s0:s1] = P.t()
@@ -126,7 +132,8 @@ class ChunkedElbo:
             t, eps = self._t(s0, s1)
             G = None
             for br, (base, gind, out) in enumerate(((self.fe, g_IL, dfe), (self.fx, g_I, dfx))):
-                E = probit_prob(t + base).to(F64)
+                E = probit_prob(t + base, self.erf_fp64)
+                E = E.to(F64)
                 w = torch.exp(self.rowstat[br, :, s0:s1] - self.m[br][:, None]) / self.Z[br][:, None]
                 a = (-gn * w / B).t()[..., None]                    # (s, B, 1)
                 bP = (scale[:, None] * self.rowstat[3 + 2 * br, :, s0:s1]).t()[..., None]
