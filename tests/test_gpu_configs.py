@@ -11,7 +11,8 @@
   (oracle/probit_elbo.py, pinned to the reference's own golden vectors).
 * The evaluation call at n_test_sample = 10000 (fairsoft_evaluate.py:40,72-74,
   mode 'test', no T stash, several sample tiles per batch row) against the
-  oracle.
+  oracle, and with the whole batch of 512 at L = 1024 and 4096 against the
+  fp64 restatement (tests/torch64_ref.py).
 The full-size properties of C3, C4 and C5 (shard invariance, determinism,
 finiteness) are in test_gpu_parity.py."""
 import argparse
@@ -86,5 +87,44 @@ def test_eval_10000_samples_against_oracle(L, B):
         out = mpvae.compute_loss(*t, torch.from_numpy(R).to(DEV), args)
     errs = {k: rel_err(_np(o), ref[k]) for k, o in zip(OUTS, out)}
     record(f"eval10000_L{L}_B{B}", errs)
+    for k, e in errs.items():
+        assert e <= FWD_RTOL, (k, e)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("L", [1024, 4096], ids=["c4", "c5"])
+def test_eval_10000_samples_full_batch_against_fp64_reference(L):
+    """The evaluation call (mode 'test', n_test_sample = 10000, no_grad) at the
+    headline and C5 label dims with the whole batch of 512, philox noise: all
+    8 outputs against the fp64 restatement (tests/torch64_ref.py) evaluated on
+    the noise planes the kernels read (redrawn from the same key)."""
+    from torch64_ref import ChunkedElbo
+    from mpvae_ops import HipShardBackend
+    from test_gpu_parity import _plane_noise
+    B, S, d, key = 512, 10000, 50, 777 + L
+    g = torch.Generator(device=DEV).manual_seed(L + 7)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    mus = [torch.randn((B, d), device=DEV, generator=g) * s for s in (1.0, 0.1, 1.0, 0.1)]
+    R = ((torch.rand((L, L), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
+         * (6.0 / (2 * L)) ** 0.5)
+    args = argparse.Namespace(label_dim=L, z_dim=L, n_train_sample=10, n_test_sample=S,
+                              mode="test", nll_coeff=0.1, c_coeff=200.0, mpvae_noise="philox",
+                              mpvae_seed=key)
+    with torch.no_grad():
+        out = mpvae.compute_loss(y, fe, mus[0], mus[1], fx, mus[2], mus[3], R, args)
+    got = [_np(o) for o in out]
+    del out
+    torch.cuda.empty_cache()
+    be = HipShardBackend()
+    pl = be.make_noise(be.shape(S, S, 0, B, L, L), DEV, key, 0)
+    ref = ChunkedElbo(y, fe, fx, R, _plane_noise(pl, B, S, L), S, chunk=64 if L > 1024 else 256)
+    rf = ref.forward(*mus, 0.1, 200.0)
+    del ref, pl
+    torch.cuda.empty_cache()
+    errs = {k: rel_err(o, _np(rf[k])) for k, o in zip(OUTS, got)}
+    record(f"eval10000_full_batch_L{L}_fp64ref", errs)
     for k, e in errs.items():
         assert e <= FWD_RTOL, (k, e)
