@@ -47,7 +47,7 @@ def test_fair_penalty_matches_reference(f):
     # a fp32 loss carries the fp64 value rounded once
     if loss.dtype == torch.float32:
         ltol = max(ltol, 1.2e-7)
-    assert abs(float(loss) - ref) <= ltol * abs(ref)
+    assert abs(float(loss.detach()) - ref) <= ltol * abs(ref)
     for g, r in ((gl, f["g_label_z"]), (gf, f["g_feat_z"])):
         assert np.abs(g.cpu().numpy() - r).max() <= gtol * np.abs(r).max()
 

@@ -21,18 +21,25 @@ def main(src, dst, note):
     for line in open(src):
         rec = json.loads(line)
         errs = rec["errs"]
-        fwd = [v for k, v in errs.items() if not is_grad(k)]
-        grad = [v for k, v in errs.items() if is_grad(k)]
+        # d*_ref_*: the reference's own spread (an fp32 variant of the fp64
+        # restatement against it), recorded beside the kernels' errors
+        spread = [v for k, v in errs.items() if "_ref_" in k]
+        errs_k = {k: v for k, v in errs.items() if "_ref_" not in k}
+        fwd = [v for k, v in errs_k.items() if not is_grad(k)]
+        grad = [v for k, v in errs_k.items() if is_grad(k)]
         c = cases.setdefault(rec["test"], {"fwd_max": None, "grad_max": None, "errs": {}})
         if fwd:
             c["fwd_max"] = max(fwd + ([c["fwd_max"]] if c["fwd_max"] is not None else []))
         if grad:
             c["grad_max"] = max(grad + ([c["grad_max"]] if c["grad_max"] is not None else []))
+        if spread:
+            c["ref_spread_max"] = max(spread + [c.get("ref_spread_max", 0.0)])
         for k, v in errs.items():
             c["errs"][k] = max(v, c["errs"].get(k, v))
     out = {"source": note,
            "metric": "normwise max|a-b|/max|b| per output tensor (tests/tolerances.py rel_err); "
                      "fwd_max / grad_max: max over the case's forward / gradient tensors "
+                     "(kernel errors; ref_spread_max: the reference's own fp32 spread, keys d*_ref_*) "
                      "(keys d*, grad*, param_* are gradients)",
            "cases": cases}
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
