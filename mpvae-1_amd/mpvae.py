@@ -227,6 +227,21 @@ def _noise_source(args, n_sample, B, z, shard, device):
     raise ValueError(f"unknown args.mpvae_noise {mode!r} (torch_cpu | philox | tensor)")
 
 
+def _empty_batch(fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar, R, args):
+    """compute_loss of a batch of 0 rows, as the reference evaluates it: its
+    means over the batch are NaN (mpvae.py:147, 190, 199-200) and indiv_prob*
+    are (0, L) (:203-204); autograd reaches the same leaves, with empty
+    gradients and a zero one for r_sqrt_sigma (an optimizer steps on it as on
+    the reference's).  There is nothing to compute, so no kernel runs."""
+    nan = torch.full((), float("nan"), dtype=torch.float32, device=fe_out.device)
+    zr = (R.sum() * 0).float()
+    ze, zx = fe_out.sum() * 0 + zr, fx_out.sum() * 0 + zr
+    nll, nll_x, c, c_x = nan + ze, nan + zx, nan + ze, nan + zx
+    kl = nan + (fe_mu.sum() + fe_logvar.sum() + fx_mu.sum() + fx_logvar.sum()) * 0
+    total = (nll + nll_x) * args.nll_coeff + (c + c_x) * args.c_coeff + kl * 1.1
+    return (total, nll, nll_x, c, c_x, kl, fx_out.float() * 0 + zr, fe_out.float() * 0 + zr)
+
+
 def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
                  r_sqrt_sigma, args):
     """Multivariate-probit ELBO of reference mpvae.py:145-210 (8-tuple)."""
@@ -237,6 +252,12 @@ def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar
     if r_sqrt_sigma.dim() != 2 or r_sqrt_sigma.shape[1] != z:
         raise ValueError(f"r_sqrt_sigma must be (label_dim, z_dim={z}), "
                          f"got {tuple(r_sqrt_sigma.shape)}")
+    if n_sample <= 0:
+        # the reference's max over an empty sample axis (mpvae.py:188)
+        raise IndexError(f"n_sample = {n_sample}: the Monte-Carlo sample axis is empty")
+    if B == 0:
+        return _empty_batch(fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar, r_sqrt_sigma,
+                            args)
     shard = mpvae_dist.shard_for(args, n_sample)
     noise, kw = _noise_source(args, n_sample, B, z, shard, fe_out.device)
     cfg = ElboConfig(n_sample, shard.S_local, shard.s_offset, args.nll_coeff, args.c_coeff,

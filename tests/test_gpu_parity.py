@@ -718,3 +718,51 @@ def test_inplace_total_and_partial_outputs():
     assert rel_err(_np(t2["fx_out"].grad), rg["fx_out"]) <= GRAD_RTOL
     assert float(t2["fe_out"].grad.abs().max()) == 0.0
     assert t2["fe_mu"].grad is None or float(t2["fe_mu"].grad.abs().max()) == 0.0
+
+
+def test_empty_inputs_match_reference_record():
+    """A batch of 0 rows and an empty sample axis behave as the reference's
+    compute_loss does (tests/golden/edge_cases.json, recorded from it by
+    tests/golden/make_golden_edge.py): NaN scalars and (0, L) indiv_prob*,
+    with gradients reaching exactly the reference's inputs (empty, and zero
+    for r_sqrt_sigma) for each output alone; n_sample = 0 raises IndexError."""
+    import json
+    import os
+    rec = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "edge_cases.json")))
+    L, z, d = rec["L"], rec["z"], rec["d"]
+    names = ["fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar", "r_sqrt_sigma"]
+
+    def inputs(B):
+        leaves = [torch.randn(B, n, device=DEV).requires_grad_() for n in (L, d, d, L, d, d)]
+        R = (torch.rand(L, z, device=DEV, dtype=torch.float64) - 0.5).requires_grad_()
+        y = torch.zeros(B, L, device=DEV)
+        if B:
+            y[:, 0] = 1
+        return y, leaves + [R]
+
+    def args(S, mode):
+        return argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
+                                  mode=mode, nll_coeff=rec["nll_coeff"], c_coeff=rec["c_coeff"])
+
+    for mode, case in rec["empty_batch"].items():
+        y, leaves = inputs(0)
+        out = mpvae.compute_loss(y, *leaves, args(4, mode))
+        for o, want in zip(out, case["outputs"]):
+            assert str(o.dtype).replace("torch.", "") == want["dtype"]
+            assert list(o.shape) == want["shape"]
+            assert bool(o.dim() == 0 and torch.isnan(o).item()) == want["nan"]
+        for i, want in enumerate(case.get("grads_per_output", [])):
+            y, leaves = inputs(0)
+            mpvae.compute_loss(y, *leaves, args(4, mode))[i].sum().backward()
+            for n, v in zip(names, leaves):
+                if want[n] is None:
+                    assert v.grad is None, (i, n)
+                    continue
+                assert v.grad is not None, (i, n)
+                assert list(v.grad.shape) == want[n]["shape"], (i, n)
+                assert str(v.grad.dtype).replace("torch.", "") == want[n]["dtype"], (i, n)
+                assert bool((v.grad == 0).all().item()) == want[n]["zero"], (i, n)
+    assert rec["zero_samples_raises"] == "IndexError"
+    y, leaves = inputs(3)
+    with pytest.raises(IndexError):
+        mpvae.compute_loss(y, *leaves, args(0, "train"))

@@ -422,3 +422,25 @@ def test_fused_reparam_passthrough_grads_bit_equal():
     out[2].clamp_(-1.0, 1.0)
     (out[2].sum() + out[0].sum()).backward()
     assert torch.isfinite(leaves[0].grad).all()
+
+
+@pytest.mark.parametrize("linear", ["hip", "torch"])
+def test_empty_batch_forward_and_backward(linear):
+    """A batch of 0 rows through VAE.forward (train and eval) and compute_loss
+    and back: the reference's nn.Linear / randn_like / compute_loss give (0, n)
+    outputs, NaN losses and zero parameter gradients (tests/golden/edge_cases.json
+    for compute_loss); no kernel may be launched with an empty grid."""
+    args = _args(mpvae_linear=linear)
+    model = _seeded_model(args).to(DEV)
+    for train in (True, False):
+        model.train(train)
+        out = model(torch.zeros(0, 6, device=DEV), torch.zeros(0, 20, device=DEV))
+        assert [tuple(o.shape) for o in out] == [(0, 6), (0, 8), (0, 8), (0, 6), (0, 8), (0, 8)]
+        if train:
+            loss = mpvae.compute_loss(torch.zeros(0, 6, device=DEV), *out, model.r_sqrt_sigma,
+                                      args)
+            assert torch.isnan(loss[0]).item()
+            loss[0].backward()
+            torch.cuda.synchronize()
+            for n, p in model.named_parameters():
+                assert p.grad is None or not p.grad.any(), n
