@@ -70,7 +70,7 @@ def test_fair_penalty_training_size_against_oracle(norm):
     rl, rc, rgl, rgf = of.fair_penalty(f["label_z"], f["feat_z"], labels, sens, dists, norm, 0.5)
     assert int(count) == rc
     assert loss.dtype == torch.float64
-    assert abs(float(loss) - rl) <= 1e-10 * abs(rl)
+    assert abs(float(loss.detach()) - rl) <= 1e-10 * abs(rl)
     for g, r in ((gl, rgl), (gf, rgf)):
         assert np.abs(g.cpu().numpy() - r).max() <= 1e-6 * np.abs(r).max()
 
