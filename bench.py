@@ -36,6 +36,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import mpvae  # noqa: E402
+import mpvae_dist  # noqa: E402
 import mpvae_hip as H  # noqa: E402
 import mpvae_launch  # noqa: E402
 
@@ -48,6 +49,11 @@ F16_MFMA_PEAK = 2.5e15      # MI355X_MICROARCH.md: dense BF16/F16 MFMA
 PEAKS = {"f16x3": (F16_MFMA_PEAK / 3.0, "f16x3 MFMA: dense f16 peak / 3"),
          "f32": (FP32_MFMA_PEAK, "f32 MFMA")}
 HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec
+# VALU ceiling (MI355X_MICROARCH.md: 157.3 TFLOPS fp32 vector = 256 CUs x 4
+# SIMD-32 x 32 lanes x 2.4 GHz x 2 flop per FMA): one lane-instruction per lane
+# per cycle, 78.6e12 lane-instructions/s.  A packed fp32 op (v_pk_*) counts as
+# one lane-instruction, like the counter (SQ_INSTS_VALU) it is measured with.
+VALU_PEAK = FP32_MFMA_PEAK / 2.0
 
 # name: (L, z, B, n_sample (total under strong scaling, per GPU under weak), d,
 #        nll_coeff, c_coeff)
@@ -57,6 +63,12 @@ CONFIGS = {
     "c4": (1024, 1024, 512, 4096, 50, 0.1, 200.0),
     "c5": (4096, 4096, 512, 8192, 50, 0.1, 200.0),
 }
+# default (timed steps, warm-up steps) per config: 200 steps keep the C2-C4
+# runs several seconds of GPU work; C5 (~0.7 s per step on one GPU) takes 10
+DEFAULT_STEPS = {"c2": (200, 5), "c3": (200, 5), "c4": (200, 5), "c5": (10, 2)}
+# the probit kernels of the small configurations (L, z <= 128) are VALU-bound
+# (SURVEY.md section 8(d)): their roofline is the VALU ceiling
+SMALL_LZ = 128
 
 
 def log(*a):
@@ -161,9 +173,12 @@ def graph_steps(y, leaves, args, warmup, steps):
     return out, time.perf_counter() - t0
 
 
-def roofline(times, S_local, B, L, z, steps, gemm):
+def roofline(times, S_local, B, L, z, steps, gemm, valu=None):
     """Dominant kernel's achieved rate vs its bound, from in-library HIP events.
-    GEMM work is the algorithmic fp32 GEMM (2*S*B*L*z flops per launch)."""
+    GEMM work is the algorithmic fp32 GEMM (2*S*B*L*z flops per launch).  With
+    L, z <= SMALL_LZ the kernels are VALU-bound: `valu` ({kernel tag: VALU
+    lane-instructions per launch}, from a committed PMC profile of the same
+    config) prices the dominant kernel against VALU_PEAK instead."""
     mfma_peak, peak_note = PEAKS[gemm]
     work = {  # algorithmic work per launch
         "probit_fwd": ("mfma", 2.0 * S_local * B * L * z, mfma_peak, "TFLOP/s"),
@@ -174,6 +189,25 @@ def roofline(times, S_local, B, L, z, steps, gemm):
     dom = max(times, key=lambda k: times[k][1])
     n, ms = times[dom]
     avg_s = ms / n / 1e3
+    small = L <= SMALL_LZ and z <= SMALL_LZ
+    if small:
+        # VALU-bound: achieved lane-instructions/s of the dominant kernel
+        per = (valu or {}).get(dom)
+        pk = VALU_PEAK / 1e12
+        achieved = per / avg_s / 1e12 if per else None
+        res = {"kernel": dom, "bound": "valu", "achieved": achieved, "peak": pk,
+               "unit": "Tlane-instr/s", "frac": achieved / pk if achieved else None,
+               "traffic": None, "avg_ms": round(avg_s * 1e3, 4),
+               "peak_basis": "VALU: 157.3 TFLOPS fp32 vector / 2 = one lane-instruction per "
+                             "lane per cycle at 2.4 GHz (packed ops count once, as in "
+                             "SQ_INSTS_VALU)"}
+        if valu:  # the whole step: every profiled kernel's lane-instructions
+            tot = sum(valu.get(k, 0.0) * times[k][0] for k in times) / steps
+            step_s = sum(v[1] for v in times.values()) / steps / 1e3
+            res["step_valu_frac"] = tot / step_s / VALU_PEAK
+        res["ms_per_step_by_op"] = {k: round(v[1] / steps, 4) for k, v in
+                                    sorted(times.items(), key=lambda kv: -kv[1][1])}
+        return res
     if dom in work:
         bound, per_launch, peak, unit = work[dom]
         scale = 1e12 if unit == "TFLOP/s" else 1e9
@@ -189,6 +223,20 @@ def roofline(times, S_local, B, L, z, steps, gemm):
             "frac": frac, "traffic": None, "peak_basis": peak_note if bound == "mfma" else
             "HBM3E spec", "avg_ms": round(avg_s * 1e3, 4),
             "ms_per_step_by_op": breakdown}
+
+
+def pmc_valu(config):
+    """{kernel tag: VALU lane-instructions per launch} from the newest committed
+    PMC summary of this config that holds them (tools/valu_summary.py:
+    (SQ_INSTS_VALU - SQ_INSTS_MFMA) x 64 per launch), with its path."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))[::-1]:
+        ks = json.load(open(f)).get("kernels", {})
+        v = {k: d["valu_lane_insts_per_launch"] for k, d in ks.items()
+             if d.get("valu_lane_insts_per_launch")}
+        if v:
+            return v, os.path.relpath(f, ROOT)
+    return None, None
 
 
 def pmc_traffic(config, kernel):
@@ -275,8 +323,8 @@ def cpu_baseline(L, z, B, d, S_cpu, reps, device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None, help="default: DEFAULT_STEPS[config]")
+    ap.add_argument("--warmup", type=int, default=None, help="default: DEFAULT_STEPS[config]")
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=int, default=2)
@@ -297,6 +345,10 @@ def main():
     ap.add_argument("--n-sample", type=int, default=None,
                     help="override the config's n_sample (train mode)")
     cli = ap.parse_args()
+    if cli.steps is None:
+        cli.steps = DEFAULT_STEPS[cli.config][0]
+    if cli.warmup is None:
+        cli.warmup = DEFAULT_STEPS[cli.config][1]
 
     if mpvae_launch.needs_spawn(cli.gpus):
         # plain `python bench.py --gpus N`: N rank processes, started before
@@ -331,6 +383,9 @@ def main():
     torch.cuda.synchronize()
     lib.mpv_timing_enable(1)
     lib.mpv_timing_reset()
+    comm = mpvae_dist.COMM_TIMER
+    comm.reset()
+    comm.enabled = dist.is_initialized()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
@@ -342,7 +397,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     lib.mpv_timing_enable(0)
+    comm.enabled = False
     times = H.kernel_times()
+    comm_by_op = comm.summary() if dist.is_initialized() else None
     graph_note = None
     if cli.graph:
         if world > 1 or forced:
@@ -357,10 +414,31 @@ def main():
         elapsed = float(t)
     finite = bool(torch.isfinite(out[0]).item())
     value = S_total * B * L * cli.steps / elapsed
-    rl = roofline(times, S_local, B, L, z, cli.steps, cli.gemm)
     prof_key = cli.config if cli.mode == "train" else cli.config + "eval"
+    valu, valu_src = pmc_valu(prof_key)
+    rl = roofline(times, S_local, B, L, z, cli.steps, cli.gemm, valu)
+    if rl["bound"] == "valu":
+        rl["valu_source"] = valu_src
     rl["traffic"], rl["traffic_source"] = pmc_traffic(prof_key, rl["kernel"])
     rl["rocprof_avg_ms"] = trace_avg_ms(prof_key, rl["kernel"])
+    # collectives of the sample-shard exchange (ms per step) and every rank's
+    # per-op kernel times: a multi-GPU line explains its own scaling loss
+    comm_ms, ranks = None, None
+    if comm_by_op is not None:
+        per_step = {op: {k: (round(v / cli.steps, 4) if isinstance(v, float) else v)
+                         for k, v in d.items()} for op, d in comm_by_op.items()}
+        dev_ms = sum(d["device_ms"] or 0.0 for d in comm_by_op.values()) / cli.steps
+        host_ms = sum(d["host_ms"] for d in comm_by_op.values()) / cli.steps
+        mine = {"rank": rank, "ms_per_step_by_op": rl["ms_per_step_by_op"],
+                "comm_device_ms": round(dev_ms, 4), "comm_host_ms": round(host_ms, 4),
+                "comm_by_op": per_step}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        comm_ms = {"device_max": max(r["comm_device_ms"] for r in ranks),
+                   "host_max": max(r["comm_host_ms"] for r in ranks),
+                   "note": "per step; device: CUDA events around each collective on the "
+                           "issuing stream (RCCL), host: wall clock around the call (gloo "
+                           "blocks the host)"}
 
     cpu, errs = None, None
     if rank == 0 and world == 1 and not cli.no_cpu_baseline and cli.mode == "train":
@@ -383,6 +461,9 @@ def main():
                                         if dist.is_initialized() else None)},
             "roofline": rl, "cpu_baseline": cpu, "elbo_rel_err": errs, "loss_finite": finite,
         }
+        if comm_ms is not None:
+            line["comm_ms"] = comm_ms
+            line["ranks"] = ranks
         if graph_note:
             line["graph"] = graph_note
         print(json.dumps(line), flush=True)

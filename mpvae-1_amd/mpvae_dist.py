@@ -37,8 +37,59 @@ silently.  Two guards:
     call (catches later drift, e.g. from nondeterministic MLP backward kernels),
     False never.
 """
+import time
+
 import torch
 import torch.distributed as dist
+
+
+class CommTimer:
+    """Optional timing of the exchange's collectives (bench.py --gpus N).
+
+    While enabled, every collective of SampleShardExchange.combine /
+    reduce_grads is bracketed by CUDA events on the current stream (RCCL makes
+    that stream wait for the collective, so the pair spans it; for device
+    tensors these events are the device-side cost) and by a host clock (gloo
+    blocks the host until its collective is done).  Off by default: nothing
+    is recorded and no event is created on the product path."""
+
+    def __init__(self):
+        self.enabled = False
+        self.reset()
+
+    def reset(self):
+        self._events = {}  # op -> [(start, end), ...]
+        self._host = {}    # op -> seconds
+
+    def run(self, op, device, fn):
+        if not self.enabled:
+            return fn()
+        cuda = isinstance(device, torch.device) and device.type == "cuda"
+        if cuda:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+        t0 = time.perf_counter()
+        out = fn()
+        self._host[op] = self._host.get(op, 0.0) + time.perf_counter() - t0
+        if cuda:
+            b.record()
+            self._events.setdefault(op, []).append((a, b))
+        return out
+
+    def summary(self):
+        """{op: {"calls", "device_ms", "host_ms"}} (synchronizes the device)."""
+        out = {}
+        for op in sorted(set(self._events) | set(self._host)):
+            ev = self._events.get(op, [])
+            if ev:
+                ev[-1][1].synchronize()
+            out[op] = {"calls": len(ev) or None,
+                       "device_ms": sum(a.elapsed_time(b) for a, b in ev) if ev else None,
+                       "host_ms": 1e3 * self._host.get(op, 0.0)}
+        return out
+
+
+COMM_TIMER = CommTimer()
 
 
 class ReplicaMismatch(RuntimeError):
@@ -78,7 +129,8 @@ class SampleShardExchange:
         sync); an int comes back as an int."""
         if isinstance(seed, torch.Tensor):
             t = seed.detach().to(device=device, dtype=torch.int64).reshape(1).clone()
-            dist.broadcast(t, src=self._src(), group=self.group)
+            COMM_TIMER.run("seed_broadcast", t.device,
+                           lambda: dist.broadcast(t, src=self._src(), group=self.group))
             return t
         u = int(seed) & (2 ** 64 - 1)  # the 64-bit Philox key, carried as int64
         t = torch.tensor([u - 2 ** 64 if u >= 2 ** 63 else u], dtype=torch.int64, device=device)
@@ -107,13 +159,15 @@ class SampleShardExchange:
 
     def combine(self, bstat, colsum, backend):
         parts = [torch.empty_like(bstat) for _ in range(self.world)]
-        dist.all_gather(parts, bstat.contiguous(), group=self.group)
+        COMM_TIMER.run("combine_all_gather", bstat.device,
+                       lambda: dist.all_gather(parts, bstat.contiguous(), group=self.group))
         bstat_global = backend.combine_bstats(torch.stack(parts))
-        dist.all_reduce(colsum, group=self.group)
+        COMM_TIMER.run("combine_all_reduce", colsum.device,
+                       lambda: dist.all_reduce(colsum, group=self.group))
         return bstat_global, colsum
 
     def reduce_grads(self, flat):
-        dist.all_reduce(flat, group=self.group)
+        COMM_TIMER.run("reduce_grads", flat.device, lambda: dist.all_reduce(flat, group=self.group))
         return flat
 
 

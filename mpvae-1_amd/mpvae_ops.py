@@ -70,12 +70,25 @@ class HipShardBackend:
     """Per-shard arithmetic on the GPU through the C ABI.
 
     gemm="f16x3" (default): the two noise GEMMs run on the f16 matrix cores
-    with 3xf16 split operands (~fp32 accuracy); gemm="f32": exact fp32 MFMA."""
+    with 3xf16 split operands (~fp32 accuracy); gemm="f32": exact fp32 MFMA.
 
-    def __init__(self, gemm="f16x3"):
+    poison=True (tests and tools/repeat_probe.py only): every output and
+    workspace buffer of forward_local / backward_local is filled with NaN bytes
+    (0xFF) before the launch, so a write the kernels skip or lose shows up as a
+    NaN instead of hiding behind the identical bytes the caching allocator
+    hands back from an earlier launch."""
+
+    def __init__(self, gemm="f16x3", poison=False):
         if gemm not in GEMMS:
             raise ValueError(f"gemm must be one of {sorted(GEMMS)} (got {gemm!r})")
         self.gemm = GEMMS[gemm]
+        self.poison = bool(poison)
+
+    def _buf(self, shape, device, dtype):
+        t = torch.empty(shape, device=device, dtype=dtype)
+        if self.poison:
+            t.view(torch.uint8).fill_(0xFF)  # all-ones words: NaN in fp32 and fp64
+        return t
 
     def shape(self, S_local, S_total, s_offset, B, L, z):
         return H.Shape(S_local, S_total, s_offset, B, L, z)
@@ -158,12 +171,13 @@ class HipShardBackend:
         dev = y.device
         S, B, L = shape.S_local, shape.B, shape.L
         # rows padded to 4 floats (ABI v5: 16-B aligned rows for the element pass)
-        T = torch.empty((B, S, (L + 3) // 4 * 4), device=dev, dtype=torch.float32) if keep_T else None
-        rowstat = torch.empty((6, B, S), device=dev, dtype=torch.float32)
-        bstat = torch.empty((6, B), device=dev, dtype=torch.float32)
-        colsum = torch.empty((2, B, L), device=dev, dtype=torch.float32)
+        f32 = torch.float32
+        T = self._buf((B, S, (L + 3) // 4 * 4), dev, f32) if keep_T else None
+        rowstat = self._buf((6, B, S), dev, f32)
+        bstat = self._buf((6, B), dev, f32)
+        colsum = self._buf((2, B, L), dev, f32)
         nbytes = lib.mpv_fwd_workspace_bytes(shape)
-        ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
+        ws = self._buf((max(nbytes, 1),), dev, torch.uint8)
         if self.gemm == H.GEMM_F16X3:
             ops = (None, None, Rop.c(), eps.c())
         else:
@@ -207,13 +221,13 @@ class HipShardBackend:
         n_fe = 2 * B * L
         dR64 = None
         if want_dR and dR_dtype == torch.float64:
-            dR64 = torch.empty((L, z), device=dev, dtype=torch.float64)
+            dR64 = self._buf((L, z), dev, torch.float64)
         with_32 = want_dR and dR64 is None
-        flat = torch.empty((n_fe + (L * z if with_32 else 0),), device=dev, dtype=torch.float32)
+        flat = self._buf((n_fe + (L * z if with_32 else 0),), dev, torch.float32)
         dfe_dfx = flat[:n_fe].view(2, B, L)
         dR = flat[n_fe:].view(L, z) if with_32 else dR64
         nbytes = lib.mpv_bwd_workspace_bytes(shape, self.gemm)
-        ws = torch.empty((max(nbytes, 1),), device=dev, dtype=torch.uint8)
+        ws = self._buf((max(nbytes, 1),), dev, torch.uint8)
         eps = saved["eps"]
         eps_ops = (None, eps.c()) if self.gemm == H.GEMM_F16X3 else (H.ptr(eps), H.Split16())
         kl_outs, kl_ref = None, None

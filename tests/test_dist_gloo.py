@@ -152,3 +152,53 @@ def test_replica_contract_is_enforced():
     for rank, seeds, outcome in results:
         assert seeds == (1000, 2 ** 64 - 1, 7000, (1,), "torch.int64"), (rank, seeds)
         assert outcome == ["ok", "mismatch", "ok"], (rank, outcome)
+
+
+def _comm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mpvae_dist
+        from golden_io import fixtures
+        from oracle_backend import OracleShardBackend
+        f = next(f for f in fixtures() if f.name == "f1_l38")
+        S_local, s_off = split_samples(f.S, world, rank)
+        t = {k: torch.from_numpy(f[k].copy()).requires_grad_(k != "y") for k in
+             ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar",
+              "r_sqrt_sigma"]}
+        noise = torch.from_numpy(f["noise"][s_off:s_off + S_local].copy())
+        timer = mpvae_dist.COMM_TIMER
+        timer.reset()
+        timer.enabled = True
+        for _ in range(2):
+            cfg = ElboConfig(f.S, S_local, s_off, f.nll_coeff, f.c_coeff,
+                             backend=OracleShardBackend(), exchange=SampleShardExchange())
+            out = ProbitELBO.apply(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
+                                   t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], noise, cfg)
+            out[0].backward()
+        timer.enabled = False
+        q.put((rank, timer.summary()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_timer_records_every_collective():
+    """bench.py --gpus N reports comm_ms from mpvae_dist.COMM_TIMER: with the
+    timer on, each collective of the exchange is recorded once per call (host
+    clock; CPU tensors have no device events), and nothing when it is off."""
+    import mpvae_dist
+    assert not mpvae_dist.COMM_TIMER.enabled
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, summ in results:
+        assert set(summ) == {"combine_all_gather", "combine_all_reduce", "reduce_grads"}, summ
+        for op, d in summ.items():
+            assert d["device_ms"] is None and d["host_ms"] > 0.0, (rank, op, d)

@@ -57,3 +57,26 @@ def test_chunked_torch64_matches_numpy_oracle(L, z, B, S, chunk, degenerate, wit
                     None if g_IL is None else torch.from_numpy(g_IL))
     for k in ("fe_out", "fx_out", "r_sqrt_sigma"):
         assert rel_err(g[k].numpy(), rg[k]) <= 2e-7, k
+
+
+def test_external_t_source_reproduces_own_t():
+    """t_src (the reference's formulas on another implementation's t, used by
+    the full-size GPU tests on the product's T stash): fed the restatement's
+    own fp64-accumulated t, chunk by chunk, it gives the same results bit for
+    bit; fed the fp32-GEMM t, the same as t_fp32=True."""
+    L, z, B, S = 40, 24, 6, 30
+    inp, noise = _case(L, z, B, S, 8, 7)
+    t = {k: torch.from_numpy(v) for k, v in inp.items()}
+    nz = torch.from_numpy(noise)
+    mk = lambda **kw: ChunkedElbo(t["y"], t["fe_out"], t["fx_out"], t["r_sqrt_sigma"],
+                                  lambda a, b: nz[a:b], S, 8, **kw)
+    for kw in ({}, {"t_fp32": True}):
+        own = mk(**kw)
+        ext = mk(t_src=lambda a, b, o=own: o._t(a, b)[0])
+        mus = (t["fe_mu"], t["fe_logvar"], t["fx_mu"], t["fx_logvar"], 0.1, 200.0)
+        fa, fb = own.forward(*mus), ext.forward(*mus)
+        for k in OUTS:
+            assert torch.equal(fa[k], fb[k]), (kw, k)
+        ga, gb = own.backward(0.1, 200.0), ext.backward(0.1, 200.0)
+        for k in ("fe_out", "fx_out", "r_sqrt_sigma"):
+            assert torch.equal(ga[k], gb[k]), (kw, k)

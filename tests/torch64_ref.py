@@ -53,7 +53,8 @@ class ChunkedElbo:
     samples [s0, s1) on the inputs' device (it is called twice per chunk:
     forward and backward, and must return the same values)."""
 
-    def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False, erf_fp64=False):
+    def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False, erf_fp64=False,
+                 t_src=None):
         self.y, self.fe, self.fx = y.to(F32), fe_out.to(F32), fx_out.to(F32)
         self.Rt = R.to(F32).to(F64).t().contiguous()          # R.T.float() (mpvae.py:165)
         self.noise, self.S, self.chunk = noise, int(S), int(chunk)
@@ -62,6 +63,12 @@ class ChunkedElbo:
         # measures how far fp32 arithmetic alone moves the results
         self.t_fp32 = bool(t_fp32)
         self.erf_fp64 = bool(erf_fp64)
+        # t_src(s0, s1) -> (s1-s0, B, L) float32: t supplied from outside (e.g.
+        # the product's own T stash) instead of computed here -- the
+        # reference's formulas evaluated on another implementation's t, to
+        # separate what t's rounding does to the gradients from what the
+        # arithmetic after t does
+        self.t_src = t_src
         self.pos, self.neg, self.n = label_sets(self.y)
         self.y64 = self.y.to(F64)
 
@@ -72,6 +79,8 @@ class ChunkedElbo:
     def _t(self, s0, s1):
         eps = self.noise(s0, s1)
         B, z = eps.shape[1], eps.shape[2]
+        if self.t_src is not None:
+            return self.t_src(s0, s1).to(F32), eps
         if self.t_fp32:
             t = eps.to(F32).reshape(-1, z) @ self.Rt.to(F32)
             return t.reshape(s1 - s0, B, -1), eps

@@ -9,6 +9,13 @@ the bytes of a wide (16 B/lane) coalesced read -> x2; WRITE_SIZE is exact for
 16 B/lane stores.  Both counters are KiB.  All loads/stores of the kernels
 summarised here are 16 B/lane (float4) except where noted in DESIGN.md.
 
+A `valu` pass (tools/profile.sh STEPS=valu: SQ_INSTS_VALU, SQ_INSTS_MFMA,
+GRBM_GUI_ACTIVE), when present, adds per kernel the VALU lane-instructions per
+launch ((SQ_INSTS_VALU - SQ_INSTS_MFMA) x 64: wave-instructions of 64 lanes;
+the counter counts MFMAs as VALU) and the effective clock (GRBM_GUI_ACTIVE / 8
+XCDs / trace duration), and the whole step's VALU lane-instructions -- bench.py
+prices the VALU-bound small configurations (L, z <= 128) with them.
+
 usage: python tools/pmc_summary.py gpurun_out/prof/c4 profiles r01_c4
 """
 import csv
@@ -66,11 +73,17 @@ def main(src, dst, tag):
         per.setdefault(short(r["Kernel_Name"]), []).append(
             (int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
     last = {k: [d for _, d in sorted(v)][-timed:] for k, v in per.items()}
-    fetch = counters(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write = counters(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
+    def opt(step, counter):
+        f = os.path.join(src, step, f"{step}_counter_collection.csv")
+        return counters(f, counter) if os.path.exists(f) else {}
+
+    fetch = opt("fetch", "FETCH_SIZE")
+    write = opt("write", "WRITE_SIZE")
+    valu, mfma, grbm = opt("valu", "SQ_INSTS_VALU"), opt("valu", "SQ_INSTS_MFMA"), \
+        opt("valu", "GRBM_GUI_ACTIVE")
     out = {"source": src, "note": "bytes per launch; fetch corrected x2 (gfx950 FETCH_SIZE "
                                   "reports half of 16B/lane reads)", "kernels": {}}
-    for k in sorted(set(fetch) | set(write)):
+    for k in sorted(set(fetch) | set(write) | set(valu)):
         f_kib, w_kib = fetch.get(k), write.get(k)
         hbm = None
         if f_kib is not None and w_kib is not None:
@@ -81,11 +94,30 @@ def main(src, dst, tag):
                              "avg_ms_trace_timed_steps": sum(lt) / len(lt) if lt else None,
                              "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                              "hbm_bytes_per_launch": hbm}
+        if k in valu:
+            lanes = 64.0 * (valu[k] - mfma.get(k, 0.0))
+            d = dur.get(k, (None, None))[1]
+            out["kernels"][k].update(
+                valu_lane_insts_per_launch=lanes, mfma_insts_per_launch=mfma.get(k),
+                clock_ghz=(grbm[k] / 8.0 / (d * 1e6) if k in grbm and d else None))
     # aliases under the timing tags bench.py reports (e.g. probit_fwd16 -> probit_fwd)
     for k in list(out["kernels"]):
         t = tag_of(k)
         if t is not None and t not in out["kernels"]:
             out["kernels"][t] = dict(out["kernels"][k], kernel=k)
+    if valu:
+        # the whole step: every mpv kernel's VALU lane-instructions per forward launch
+        tot = {}
+        f = os.path.join(src, "valu", "valu_counter_collection.csv")
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA") and \
+                    r["Kernel_Name"].startswith(("void mpv::", "mpv::")):
+                sgn = 1.0 if r["Counter_Name"] == "SQ_INSTS_VALU" else -1.0
+                tot["all"] = tot.get("all", 0.0) + sgn * 64.0 * float(r["Counter_Value"])
+        nfwd = sum(1 for r in csv.DictReader(open(f)) if r["Counter_Name"] == "SQ_INSTS_VALU"
+                   and short(r["Kernel_Name"]).startswith("probit_fwd"))
+        if nfwd:
+            out["valu_lane_insts_per_step"] = tot.get("all", 0.0) / nfwd
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -2,6 +2,7 @@
 # rocprofv3 evidence for the bench workload (run on the GPU box via gpurun):
 #   1. kernel trace + stats (per-kernel durations)
 #   2. PMC FETCH_SIZE pass, 3. PMC WRITE_SIZE pass (separate passes: TCC slots)
+#   4. (STEPS="... valu") SQ_INSTS_VALU / SQ_INSTS_MFMA / GRBM_GUI_ACTIVE of every kernel
 # Outputs under gpurun_out/prof/<tag>/; copy the summaries into profiles/.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -26,6 +27,7 @@ for s in $STEPS; do
     trace) run trace --kernel-trace --stats ;;
     fetch) run fetch --pmc FETCH_SIZE --kernel-include-regex "$KRE" ;;
     write) run write --pmc WRITE_SIZE --kernel-include-regex "$KRE" ;;
+    valu) run valu --pmc SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-include-regex "${VKRE:-mpv::}" ;;
   esac
 done
 find "$OUT" -name "*.csv" | head -20

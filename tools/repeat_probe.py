@@ -1,5 +1,10 @@
 """Count forward launches whose row statistics differ (bitwise) from the first
-launch on identical inputs: python tools/repeat_probe.py B S L z runs"""
+launch on identical inputs: python tools/repeat_probe.py B S L z runs
+
+Every output and workspace buffer is NaN-poisoned before each launch
+(HipShardBackend(poison=True); PROBE_NO_POISON=1 turns it off), so a store
+that is skipped or lost shows as a NaN (counted separately) instead of
+hiding behind the bytes an identical earlier launch left behind."""
 import os
 import sys
 
@@ -20,7 +25,7 @@ fx = torch.randn((B, L), device=DEV, generator=g)
 if os.environ.get("PROBE_SWAP") == "1":  # the two branches' means exchanged
     fe, fx = fx, fe
 R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.03
-be = HipShardBackend()
+be = HipShardBackend(poison=os.environ.get("PROBE_NO_POISON") != "1")
 shape = be.shape(S, S, 0, B, L, z)
 Rop = be.prepare_R(R)
 eps = be.make_noise(shape, DEV, 42, 0)
@@ -31,7 +36,7 @@ bwd = os.environ.get("PROBE_BWD") == "1"
 def one(keep):
     loc = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=keep or bwd)
     if os.environ.get("PROBE_T") == "1" and keep:  # compare the T stash too
-        return loc["rowstat"].clone(), loc["T"].clone()
+        return loc["rowstat"].clone(), loc["T"][..., :L].clone()  # pad columns: unwritten
     if not bwd:
         return loc["rowstat"].clone(), None
     saved = dict(y=y, fe_out=fe, fx_out=fx, eps=eps, T=loc["T"], rowstat=loc["rowstat"],
@@ -41,11 +46,13 @@ def one(keep):
 
 
 first, gfirst = one(True)
-bad_runs, bad_k, bad_g = 0, set(), 0
+bad_runs, bad_k, bad_g, nan_runs = 0, set(), 0, 0
 detail = os.environ.get("PROBE_DETAIL") == "1"
 shown = 0
 for _ in range(runs):
     rs, gr = one(keep_T)
+    if not torch.isfinite(rs).all() or (gr is not None and not torch.isfinite(gr).all()):
+        nan_runs += 1  # an unwritten (still poisoned) output element
     d = rs != first
     if d.any():
         bad_runs += 1
@@ -68,6 +75,7 @@ for _ in range(runs):
             print(f"  T differs in {dt.shape[0]} elements, first {dt[:4].tolist()}", flush=True)
 torch.cuda.synchronize()
 print(f"{os.environ.get('MPVAE_HIP_LIB', 'x/default/x').split('/')[-2]} B={B} S={S} L={L}: "
-      f"keep_T={keep_T} {bad_runs}/{runs} runs differ, stats {sorted(bad_k)}"
+      f"keep_T={keep_T} {bad_runs}/{runs} runs differ, stats {sorted(bad_k)}, "
+      f"{nan_runs}/{runs} with unwritten (NaN) outputs"
       + (f"; backward/T: {bad_g}/{runs} differ" if (bwd or gfirst is not None) else ""),
       flush=True)
