@@ -129,13 +129,20 @@ struct ElemCol {
   f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total
   float y[4];
   bool soft[4];
-  float qb[4];  // d = kEh w + qb: E - 1 for y = 0 (the sign of d logp/dE folded in), E otherwise
+  float qm[4];  // d = E + qm: E - 1 for y = 0 (the sign of d logp/dE folded in), E otherwise
   float sga[4];   // e^{-5E} (y = 1) or e^{5E} as exp2(sga w) e^{-+5 C0}
   float wp[4], wn[4];  // [y = 1], [y = 0]
 };
 
 // Four elements (columns) of one row at once, step-major so that the
 // dependent packed ops of one element interleave with the others'.
+// SOFT: the block may hold soft (non 0/1) labels (a per-column branch; false:
+// no branch at all, so the four columns' chains interleave in one basic
+// block).  NANCHK: poison the row here when bP is NaN (false: the caller does
+// it with a wave-uniform test).  SOFT_RCP: a soft label's y/E - (1-y)/(1-E)
+// by hardware reciprocals (1 ulp) instead of IEEE divisions, whose
+// registers would spill the LDS-ring kernel.
+template <bool SOFT = true, bool NANCHK = true, bool SOFT_RCP = false>
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
                        f32x2 (&out)[4]) {
   f32x2 zq[4], w[4], phic[4];
@@ -145,14 +152,27 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
   const f32x2 nbP = -bP;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
+    // E in the reference's rounding order (mpvae.py:171-180: cdf = 0.5 (1 +
+    // erf) exact from w = 1 + erf, then cdf (1 - eps1) and + eps1/2 each
+    // rounded in fp32), so that near E -> 1, where one fp32 ulp of E is ~6 %
+    // of 1 - E and 1/(1 - E) weights the gradient, E is the reference's E
+    // bit for bit whenever w is (a single fma(w, kEh, C0) rounds once and
+    // moved such gradients by ~1e-3: DESIGN.md section 4, "Full C4")
+    f32x2 E;
+    {
+#pragma clang fp contract(off)
+      E = w[q] * kEh + splat2(kC0);
+    }
     // d logp / dE = y/E - (1-y)/(1-E): one reciprocal of E (y = 1) or of
-    // E - 1 (y = 0, the sign folded in), selected as kEh w + qb
-    const f32x2 d = pk_fma(w[q], splat2(kEh), splat2(c.qb[q]));
+    // E - 1 (y = 0, the sign folded in; exact for E >= 0.5)
+    const f32x2 d = E + splat2(c.qm[q]);
     const f32x2 r = f32x2{fast_rcp(d.x), fast_rcp(d.y)};
     f32x2 dE;
-    if (c.soft[q]) {
-      const f32x2 E = pk_fma(w[q], splat2(kEh), splat2(kC0));
-      const f32x2 dl = splat2(c.y[q]) / E - splat2(1.0f - c.y[q]) / (splat2(1.0f) - E);
+    if (SOFT && c.soft[q]) {
+      const f32x2 omE = splat2(1.0f) - E;
+      const f32x2 dl = SOFT_RCP ? splat2(c.y[q]) * f32x2{fast_rcp(E.x), fast_rcp(E.y)} -
+                                      splat2(1.0f - c.y[q]) * f32x2{fast_rcp(omE.x), fast_rcp(omE.y)}
+                                : splat2(c.y[q]) / E - splat2(1.0f - c.y[q]) / omE;
       dE = pk_fma(alpha, dl, c.gind[q]);
     } else {
       dE = pk_fma(alpha, r, c.gind[q]);
@@ -164,7 +184,7 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
     out[q] = dE * phic[q];
   }
   // a degenerate row poisons every label, whatever its value (reference autograd)
-  if (bP.x != bP.x || bP.y != bP.y) {
+  if (NANCHK && (bP.x != bP.x || bP.y != bP.y)) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (bP.x != bP.x) out[q].x = bP.x;
@@ -199,6 +219,34 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
   }
 }
 
+// The lane's four label columns c0 .. c0+3 of batch row b: validity and the
+// per-column constants of the element math (ElemCol).
+MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, bool (&ok)[4],
+                            ElemCol& ec) {
+  const int L = p.L;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    ok[q] = active && c < L;
+    const int64_t o = (int64_t)b * L + (ok[q] ? c : 0);
+    const float yv = ok[q] ? p.y[o] : 0.0f;
+    const float fe = ok[q] ? p.fe[o] : 0.0f;
+    const float fx = ok[q] ? p.fx[o] : 0.0f;
+    const float gi = (ok[q] && p.gI) ? p.gI[o] * p.inv_S : 0.0f;
+    const float gil = (ok[q] && p.gIL) ? p.gIL[o] * p.inv_S : 0.0f;
+    ec.base[q] = f32x2{fe, fx} * kZq;
+    ec.gind[q] = f32x2{gil, gi};
+    ec.y[q] = yv;
+    ec.soft[q] = !(yv == 0.0f || yv == 1.0f);
+    ec.qm[q] = yv == 0.0f ? -1.0f : 0.0f;  // E - 1 = -(1 - E), or E
+    const float sgx = (yv == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
+    ec.sga[q] = sgx * kEh;
+    // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
+    ec.wp[q] = yv == 1.0f ? exp2f(sgx * kC0) : 0.0f;
+    ec.wn[q] = yv == 0.0f ? exp2f(sgx * kC0) : 0.0f;
+  }
+}
+
 // Rows of T in flight per thread beyond the one computing (kElemLookahead),
 // and ONE: a block row covers all its columns (RPI == 1), so the row index and
 // the six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
@@ -218,35 +266,10 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
   const int S = p.S, B = p.B, L = p.L;
   const float gs = PLANES ? *p.g_scale : 1.0f;
 
-  float yv[4], fe[4], fx[4], gi[4], gil[4];
-  bool ok[4], soft[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = c0 + q;
-    ok[q] = active && c < L;
-    const int64_t o = (int64_t)b * L + (ok[q] ? c : 0);
-    yv[q] = ok[q] ? p.y[o] : 0.0f;
-    fe[q] = ok[q] ? p.fe[o] : 0.0f;
-    fx[q] = ok[q] ? p.fx[o] : 0.0f;
-    gi[q] = (ok[q] && p.gI) ? p.gI[o] * p.inv_S : 0.0f;
-    gil[q] = (ok[q] && p.gIL) ? p.gIL[o] * p.inv_S : 0.0f;
-    soft[q] = !(yv[q] == 0.0f || yv[q] == 1.0f);
-  }
-  f32x2 sg2[4] = {splat2(0.f), splat2(0.f), splat2(0.f), splat2(0.f)};  // (label, feature)
+  bool ok[4];
   ElemCol ec;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    ec.base[q] = f32x2{fe[q], fx[q]} * kZq;
-    ec.gind[q] = f32x2{gil[q], gi[q]};
-    ec.y[q] = yv[q];
-    ec.soft[q] = soft[q];
-    ec.qb[q] = yv[q] == 0.0f ? kC0 - 1.0f : kC0;  // E - 1 = -(1 - E), E: affine maps of w
-    const float sgx = (yv[q] == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
-    ec.sga[q] = sgx * kEh;
-    // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
-    ec.wp[q] = yv[q] == 1.0f ? exp2f(sgx * kC0) : 0.0f;
-    ec.wn[q] = yv[q] == 0.0f ? exp2f(sgx * kC0) : 0.0f;
-  }
+  elem_col_setup(p, b, c0, active, ok, ec);
+  f32x2 sg2[4] = {splat2(0.f), splat2(0.f), splat2(0.f), splat2(0.f)};  // (label, feature)
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
   if (active && c0 < p.Lc) {
@@ -312,6 +335,137 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
       }
       p.colpart[(((int64_t)sc * 2 + 0) * B + b) * L + c] = e;
       p.colpart[(((int64_t)sc * 2 + 1) * B + b) * L + c] = x;
+    }
+  }
+}
+
+// The element pass for 3xf16 planes when a block row covers 1024 columns
+// (L >= 1024: C4, C5).  T rows stream through a per-wave LDS ring by LDS-DMA
+// (global_load_lds_dwordx4: a wave moves the 1 KB of a row its own 256
+// columns need, so no wave reads another's slot and the ring needs no
+// barrier); the row's six coefficients come from an LDS copy of the block's
+// chunk.  The loop then issues no register load that hipcc must wait for --
+// its only vector-memory ops are the DMA (counted here, lds_dma16) and the two
+// G-plane stores per row -- and with SOFT false it has no divergent branch,
+// so the four columns' element math interleaves in one basic block.  (The
+// register-lookahead kernel above serialises each column's dependent packed
+// ops behind s_nop: its per-column soft-label branches split the row into
+// basic blocks the scheduler cannot interleave across, and without them hipcc
+// drains its lookahead loads every row: DESIGN.md section 3.)
+constexpr int kElemRing = 6;       // T rows in flight per wave (1 KB each)
+constexpr int kElemRingRows = 256;  // rows per sub-chunk (the coefficient copy)
+constexpr int kElemRingMinRows = 64;  // rows per block at least (plan_bwd)
+// The rows of one sub-chunk [sb, sb + nrows) for one wave; SOFT: the block
+// holds soft labels (block-uniform, so either loop is one basic block).
+template <bool SOFT>
+MPV_DEV void elem_ring_rows(const ElemParams& p, const ElemCol& ec, const bool (&ok)[4], bool live,
+                            int b, int sb, int nrows, int c0, float gs, uint32_t voff,
+                            float* myring, const float (*cf)[8], f32x2 (&sg2)[4]) {
+  constexpr int NR = kElemRing;
+  const int lane = threadIdx.x & 63;
+  const int64_t rowb = (int64_t)b * p.S + sb;
+  const char* tbase = reinterpret_cast<const char*>(p.T + rowb * p.ldT);
+  const int64_t rstride = (int64_t)p.ldT * 4;
+  auto issue = [&](int r) {  // LDS-DMA of row r (sub-chunk-relative) into its slot
+    lds_dma16(tbase + r * rstride, voff, lds_addr(myring + (r % NR) * 256));
+  };
+  const int pro = min(NR, nrows);
+  for (int r = 0; r < pro; ++r) issue(r);
+  for (int r = 0; r < nrows; ++r) {
+    // ops issued after row r's DMA: the DMAs of rows r+1 .. min(r+NR-1,
+    // last) and the two plane stores of each row max(0, r-NR+1) .. r-1;
+    // vector memory ops retire in issue order
+    wait_vmcnt_dyn(min(NR - 1, nrows - 1 - r) + 2 * min(r, NR - 1));
+    const f32x4 tv = *reinterpret_cast<const f32x4*>(myring + (r % NR) * 256 + lane * 4);
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(&cf[r][0]);
+    const f32x2 cb = *reinterpret_cast<const f32x2*>(&cf[r][4]);
+    const f32x2 alpha = f32x2{ca[0], ca[3]}, bP = f32x2{ca[1], cb[0]}, bN = f32x2{ca[2], cb[1]};
+    const float t[4] = {tv[0], tv[1], tv[2], tv[3]};
+    f32x2 g2[4];
+    d_elem2x4<SOFT, false, true>(t, ec, alpha, bP, bN, g2);
+    // a degenerate row poisons every label (the row's bP is wave-uniform)
+    if (__builtin_amdgcn_readfirstlane((bP.x != bP.x || bP.y != bP.y) ? 1 : 0)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (bP.x != bP.x) g2[q].x = bP.x;
+        if (bP.y != bP.y) g2[q].y = bP.y;
+      }
+    }
+    float G[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sg2[q] = sg2[q] + g2[q];
+      G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
+    }
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
+    const int64_t o = chunked_index(rowb + r, p.gld, live ? c0 : 0);
+    const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
+    const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
+    if (live) {  // nontemporal plane stores (the element pass -2 %, round 2)
+      __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
+      __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
+    }
+    if (r + NR < nrows) issue(r + NR);  // into the slot row r was just read from
+  }
+}
+
+__global__ __launch_bounds__(256, 4) void bwd_elem_ring_kernel(ElemParams p) {
+  constexpr int NR = kElemRing, CR = kElemRingRows;
+  __shared__ __attribute__((aligned(16))) float ring[4][NR][256];  // [wave][slot][1 KB]
+  __shared__ __attribute__((aligned(16))) float cf[CR][8];  // alpha, bP, bN (label, feature)
+  const int b = blockIdx.x, sc = blockIdx.y, tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = blockIdx.z * 1024 + tid * 4;
+  const int S = p.S, B = p.B, L = p.L;
+  const float gs = *p.g_scale;
+  bool ok[4];
+  ElemCol ec;
+  elem_col_setup(p, b, c0, true, ok, ec);
+  bool my_soft = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) my_soft |= ok[q] && ec.soft[q];
+  const bool soft_any = __syncthreads_or(my_soft) != 0;
+  // a wave whose first lane is past the planes' columns writes nothing and
+  // streams nothing (its lane 0 has the wave's smallest c0); in a live wave
+  // every store instruction has a live lane, so it issues (the vmcnt
+  // arithmetic of elem_ring_rows counts on that)
+  const bool wave_live = (int)(blockIdx.z * 1024 + wid * 256) < p.Lc;
+  const bool live = c0 < p.Lc;
+  const int s_begin = sc * p.rows_per_chunk;
+  const int s_end = min(S, s_begin + p.rows_per_chunk);
+  const int64_t BS = (int64_t)B * S;
+  // lanes past the row's end (L % 1024 != 0) re-read column 0 and are masked
+  const uint32_t voff = (uint32_t)((c0 < L ? c0 : 0) * 4);
+  f32x2 sg2[4] = {splat2(0.f), splat2(0.f), splat2(0.f), splat2(0.f)};
+  for (int sb = s_begin; sb < s_end; sb += CR) {  // sub-chunks of <= CR rows
+    const int nrows = min(CR, s_end - sb);
+    __syncthreads();  // the previous sub-chunk's cf reads are done
+#pragma unroll
+    for (int k = 0; k < 6; ++k)  // coef is [k][b][s] -> cf[row][k]
+      for (int r = tid; r < nrows; r += 256) cf[r][k] = p.coef[k * BS + (int64_t)b * S + sb + r];
+    __syncthreads();
+    if (!wave_live) continue;
+    if (soft_any)
+      elem_ring_rows<true>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, &ring[wid][0][0], cf, sg2);
+    else
+      elem_ring_rows<false>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, &ring[wid][0][0], cf, sg2);
+  }
+  // column sums of the block's rows -> colpart (the ring is free now)
+  __syncthreads();
+  float* cred = &ring[0][0][0];  // 256 x 8 floats (8 KB, within the ring)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    cred[tid * 8 + q] = sg2[q].x;
+    cred[tid * 8 + 4 + q] = sg2[q].y;
+  }
+  __syncthreads();
+  for (int j = tid; j < 1024; j += 256) {
+    const int c = blockIdx.z * 1024 + j;
+    if (c < L) {
+      p.colpart[(((int64_t)sc * 2 + 0) * B + b) * L + c] = cred[(j >> 2) * 8 + (j & 3)];
+      p.colpart[(((int64_t)sc * 2 + 1) * B + b) * L + c] = cred[(j >> 2) * 8 + 4 + (j & 3)];
     }
   }
 }
@@ -869,8 +1023,11 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   pl.RPI = 256 / pl.TPR;
   // s-chunks: enough blocks for several rounds of resident blocks (short tail)
   int64_t want = cdiv(8192, B * pl.nLc);
-  // but at least kElemMinRows rows per thread (block setup amortised)
-  want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * kElemMinRows));
+  // but at least kElemMinRows rows per thread (block setup amortised; the
+  // LDS-ring kernel, with its coefficient staging and ring prologue per block,
+  // kElemRingMinRows, which matters at small n_sample: the strong-scaling share)
+  const int64_t min_rows = (planes && pl.RPI == 1) ? kElemRingMinRows : kElemMinRows;
+  want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * min_rows));
   if (want < 1) want = 1;
   const int64_t max_chunks = cdiv(S, pl.RPI);
   if (want > max_chunks) want = max_chunks;
@@ -1015,8 +1172,8 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.inv_S = 1.0f / (float)shape->S_total;
   const dim3 eg(B, pl.nSc, pl.nLc);
   // t_cols rows: 16-B aligned, whole float4 reads (VEC)
-  if (want_planes && pl.RPI == 1)
-    MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, true>), eg, dim3(256), 0, st, ep);
+  if (want_planes && pl.RPI == 1)  // L >= 1024: the LDS-ring element pass
+    MPV_LAUNCH("bwd_elem", bwd_elem_ring_kernel, eg, dim3(256), 0, st, ep);
   else if (want_planes)
     MPV_LAUNCH("bwd_elem", (bwd_elem_kernel<true, true, false>), eg, dim3(256), 0, st, ep);
   else

@@ -141,9 +141,9 @@ MPV_DEV void fwd_cols_stage(float* cols, const FwdParams& p, int b, int n0, int 
 
 // The transposed kernel's layout (kColsT * BN floats): (fe, fx) pairs, then
 // y[BN], then the epilogue's per-label constants, one BN array each (so a
-// lane reads its 4 labels' values as one f32x4): qa, qb (q = qa w + qb: E for
+// lane reads its 4 labels' values as one f32x4): qa, qb (q = qa E + qb: E for
 // y = 1, 1 - E for y = 0, 1 for a pad or soft label), sga, sgb (ranking
-// exponent sg E = sga w + sgb), wpos, wneg ([y = 1], [y = 0] of a real label).
+// exponent sga E + sgb = sg E), wpos, wneg ([y = 1], [y = 0] of a real label).
 // Staged once per workgroup: the labels are the same for all its tiles.
 constexpr int kColsT = 9;
 enum { kCqa = 3, kCqb, kCsga, kCsgb, kCwpos, kCwneg };
@@ -160,10 +160,10 @@ MPV_DEV void fwd_cols_stage_t(float* cols, const FwdParams& p, int b, int n0, in
     cols[2 * BN + i] = y;
     const float sg = y == 1.0f ? -5.0f * 1.4426950408889634f : 5.0f * 1.4426950408889634f;
     const bool hard = ok && (y == 0.0f || y == 1.0f);
-    cols[kCqa * BN + i] = !hard ? 0.0f : (y == 0.0f ? -kEh : kEh);
-    cols[kCqb * BN + i] = !hard ? 1.0f : (y == 0.0f ? 1.0f - kC0 : kC0);
-    cols[kCsga * BN + i] = sg * kEh;
-    cols[kCsgb * BN + i] = sg * kC0;
+    cols[kCqa * BN + i] = !hard ? 0.0f : (y == 0.0f ? -1.0f : 1.0f);
+    cols[kCqb * BN + i] = (hard && y == 1.0f) ? 0.0f : 1.0f;  // 1 - E is exact for E >= 0.5
+    cols[kCsga * BN + i] = sg;
+    cols[kCsgb * BN + i] = 0.0f;
     cols[kCwpos * BN + i] = (ok && y == 1.0f) ? 1.0f : 0.0f;
     cols[kCwneg * BN + i] = (ok && y == 0.0f) ? 1.0f : 0.0f;
   }
@@ -293,8 +293,19 @@ MPV_DEV void fwd_colsum_epilogue(const FwdParams& p, FwdLane<TN>& ln, int b, int
 }
 
 // ------------------------------------------------------ exact fp32 mainloop
+// Kernels whose workgroups share a CU (several per CU) run one workgroup's
+// epilogue VALU beside another's MFMAs on the same SIMD; they are compiled
+// without packed fp32 (v_pk_*) instructions: in that configuration a packed
+// fp32 op has been seen to lose its low-half result now and then (the
+// round-3 128 x 128 tile, DESIGN.md section 3 "Round 5: the lost update"),
+// and the same kernel in scalar code never did (0 of 120 launches).
+#ifdef __HIP_DEVICE_COMPILE__  // a device-code target feature (the host pass has none)
+#define MPV_NO_PK_FP32 __attribute__((target("no-packed-fp32-ops")))
+#else
+#define MPV_NO_PK_FP32
+#endif
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
+__global__ MPV_NO_PK_FP32 __launch_bounds__(WM* WN * 64) void probit_fwd_kernel(FwdParams p) {
   constexpr int NT = WM * WN * 64;
   constexpr int BM = WM * TM * 16;
   constexpr int BN = WN * TN * 16;
@@ -564,8 +575,10 @@ MPV_DEV void fwd16_mfma(f32x4 (&acc)[TM][TN], const Frag16<TM, TN>& f) {
 
 // Main loop: a ring of NSTAGE stage images, NSTAGE-1 stages in flight, one
 // raw barrier per stage (the DMA stream runs across tile seams).
+// Two 4-wave workgroups share each CU (the 48-label tile, 70 KB of LDS):
+// no packed fp32 (MPV_NO_PK_FP32, above).
 template <int WM, int WN, int TM, int TN, int NSTAGE>
-__global__ __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fwd16_kernel(FwdParams p) {
+__global__ MPV_NO_PK_FP32 __launch_bounds__(WM* WN * 64, (WM * WN <= 4) ? 2 : 1) void probit_fwd16_kernel(FwdParams p) {
   constexpr int NW = WM * WN;
   constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
   constexpr int STAGE = (BM + BN) * kRowB;
@@ -735,14 +748,6 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   for (int m = 0; m < TL; ++m)
 #pragma unroll
     for (int n = 0; n < TS; ++n) acc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
-  // C0 x (number of this wave's samples that the column sums count)
-  float ecount = 0.0f;
-#pragma unroll
-  for (int n = 0; n < TS; ++n) {
-    const int sb = s0 + (sbo + n) * 16;
-    ecount += (float)max(0, min(S, sb + 16) - max(s_own, sb));
-  }
-  ecount *= kC0;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
   // (round 2: unrolled by 2, 15 VGPRs spill; fully, 95.  Round 3's compiler
@@ -789,10 +794,9 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     const f32x2 fex[4] = {f32x2{pa[0], pa[1]}, f32x2{pa[2], pa[3]}, f32x2{pb[0], pb[1]},
                           f32x2{pb[2], pb[3]}};
     const f32x4 y4 = *reinterpret_cast<const f32x4*>(cols + 2 * BN + lb);
-    // per label: the ranking exponent sg E = sga w + sgb, q = qa w + qb
+    // per label: the ranking exponent sg E = sga E + sgb, q = qa E + qb
     // selecting E (y = 1) or 1 - E (y = 0) without a select, and the
-    // positive / negative weights (w = 2 Phi(u), E = kEh w + C0:
-    // probit_w2xN_zq), staged per workgroup by fwd_cols_stage_t
+    // positive / negative weights, staged per workgroup by fwd_cols_stage_t
     const f32x4 qa = *reinterpret_cast<const f32x4*>(cols + kCqa * BN + lb);
     const f32x4 qb = *reinterpret_cast<const f32x4*>(cols + kCqb * BN + lb);
     const f32x4 sga = *reinterpret_cast<const f32x4*>(cols + kCsga * BN + lb);
@@ -816,15 +820,27 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int i = 0; i < 4; ++i) zq[i] = pk_fma(splat2(t4[i]), splat2(kZq), fex[i]);
       probit_w2xN_zq<4>(zq, w4);
+      // E in the reference's rounding order (mpvae.py:171-180: cdf = 0.5 (1 +
+      // erf) exact from w = 1 + erf, then cdf (1 - eps1) and + eps1/2 each
+      // rounded): near E -> 1, where one fp32 ulp of E is several % of 1 - E,
+      // the BCE term log(1 - E) -- and through the row's log-sum-exp weights
+      // every gradient of the batch row -- then follows the reference's E
+      // bit for bit whenever w does ("Full C4")
+      f32x2 E4[4];
+      {
+#pragma clang fp contract(off)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) E4[i] = w4[i] * kEh + splat2(kC0);
+      }
       f32x2 q[4], r[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         // BCE operand (mpvae.py:184-185): E for y = 1, 1 - E for y = 0, 1 for a pad label
-        q[i] = (i & 1) ? pk_fma_bc<1>(w4[i], qa2[i >> 1], qb2[i >> 1])
-                       : pk_fma_bc<0>(w4[i], qa2[i >> 1], qb2[i >> 1]);
+        q[i] = (i & 1) ? pk_fma_bc<1>(E4[i], qa2[i >> 1], qb2[i >> 1])
+                       : pk_fma_bc<0>(E4[i], qa2[i >> 1], qb2[i >> 1]);
         // ranking factors (mpvae.py:110-114 factorised): pos -> e^{-5E}, neg -> e^{5E}
-        const f32x2 a = (i & 1) ? pk_fma_bc<1>(w4[i], sga2[i >> 1], sgb2[i >> 1])
-                                : pk_fma_bc<0>(w4[i], sga2[i >> 1], sgb2[i >> 1]);
+        const f32x2 a = (i & 1) ? pk_fma_bc<1>(E4[i], sga2[i >> 1], sgb2[i >> 1])
+                                : pk_fma_bc<0>(E4[i], sga2[i >> 1], sgb2[i >> 1]);
         r[i] = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
       }
       // sum of the 4 labels' log-probs as ONE log of their product (log2 units,
@@ -837,7 +853,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         for (int i = 0; i < 4; ++i) {
           const float y = y4[i];
           if (n0 + lb + i < L && !(y == 0.0f || y == 1.0f)) {  // soft label: both BCE terms (q = 1)
-            const f32x2 E = pk_fma(w4[i], splat2(kEh), splat2(kC0));
+            const f32x2 E = E4[i];
             lp.x += y * __builtin_amdgcn_logf(E.x) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.x);
             lp.y += y * __builtin_amdgcn_logf(E.y) + (1.0f - y) * __builtin_amdgcn_logf(1.0f - E.y);
           }
@@ -851,7 +867,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
           pk_fma2_acc_bc<1>(wpos2[i >> 1], wneg2[i >> 1], r[i], sp[n], sn[n]);
         else
           pk_fma2_acc_bc<0>(wpos2[i >> 1], wneg2[i >> 1], r[i], sp[n], sn[n]);
-        ce[i] = pk_fma(splat2(wr), w4[i], ce[i]);  // sum E = kEh sum w + C0 count
+        ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);  // column sums of E over the wave's samples
       }
       // kEpiSampleBlocks samples at a time: bounded live ranges vs more independent chains
       if ((n + 1) % kEpiSampleBlocks == 0) __builtin_amdgcn_sched_barrier(0);
@@ -870,8 +886,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float* c = cacc + (ws * BN + lb + i) * 2;
-        c[0] += fmaf(kEh, cs[2 * i], ecount);
-        c[1] += fmaf(kEh, cs[2 * i + 1], ecount);
+        c[0] += cs[2 * i];
+        c[1] += cs[2 * i + 1];
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group

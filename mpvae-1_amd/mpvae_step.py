@@ -142,8 +142,19 @@ class DeviceStepLR:
     torch's StepLR bit for bit (the chainable ``lr * gamma`` in double when
     last_epoch is a non-zero multiple of step_size).  The optimizer's
     ``param_groups[i]["lr"]`` and the scheduler's ``last_epoch`` /
-    ``get_last_lr()`` go stale while TrainStep owns them: ``sync()`` (one host
-    sync) writes them back, e.g. before logging or ``state_dict()``."""
+    ``get_last_lr()`` would go stale while TrainStep owns them; so (ADVICE
+    r04):
+      * ``opt.state_dict()`` and ``sched.state_dict()`` sync first (an
+        optimizer state-dict pre-hook; the scheduler's method wrapped), so a
+        checkpoint holds the current lr and epoch;
+      * the scheduler's own ``step()`` raises while TrainStep owns it (the
+        reference loop's host ``scheduler.step()`` would step it twice) until
+        ``release()`` hands it back, synced;
+      * a host edit of ``param_groups[i]["lr"]`` is adopted by the device
+        state before the next step (``adopt_host_lr``, called by TrainStep: a
+        host-side comparison, no device sync), with a warning.
+    ``sync()`` (one host sync) writes the device state back on demand, e.g.
+    before logging."""
 
     def __init__(self, sched, opt):
         if type(sched) is not torch.optim.lr_scheduler.StepLR:
@@ -158,6 +169,20 @@ class DeviceStepLR:
         self.last_epoch = torch.tensor(int(sched.last_epoch), dtype=torch.int64, device=dev)
         self.step_size, self.gamma = float(sched.step_size), float(sched.gamma)
         self._epoch0 = int(sched.last_epoch)
+        self._host_lr = [float(g["lr"]) for g in opt.param_groups]  # as last synced / adopted
+        self._hook = opt.register_state_dict_pre_hook(lambda _opt: self.sync())
+        self._sched_state_dict, self._sched_step = sched.state_dict, sched.step
+
+        def state_dict():
+            self.sync()
+            return self._sched_state_dict()
+
+        def step(*a, **k):
+            raise RuntimeError("this StepLR is stepped on the device by TrainStep after every "
+                               "applied update (fairsoft_train.py:142-145); do not call "
+                               "scheduler.step() as well -- TrainStep.release_scheduler() hands "
+                               "it back")
+        sched.state_dict, sched.step = state_dict, step
 
     def sync(self):
         """Copy the device lr / last_epoch into the optimizer and the scheduler."""
@@ -169,6 +194,25 @@ class DeviceStepLR:
         self.sched._last_lr = list(lrs)
         self.sched._step_count += epoch - self._epoch0
         self._epoch0 = epoch
+        self._host_lr = list(lrs)
+        return lrs
+
+    def adopt_host_lr(self):
+        """A param group's lr changed on the host since the last sync: the
+        device lr takes it (host compare, non-blocking copy; no device sync)."""
+        now = [float(g["lr"]) for g in self.opt.param_groups]
+        if now != self._host_lr:
+            import warnings
+            warnings.warn("optimizer param_groups lr edited on the host while TrainStep owns "
+                          "the StepLR: the device lr adopts the new value", stacklevel=3)
+            self.lr.copy_(torch.tensor(now, dtype=torch.float64), non_blocking=False)
+            self._host_lr = now
+
+    def release(self):
+        """Sync, then hand the scheduler and optimizer back to host control."""
+        lrs = self.sync()
+        self._hook.remove()
+        self.sched.state_dict, self.sched.step = self._sched_state_dict, self._sched_step
         return lrs
 
 
@@ -282,8 +326,18 @@ class TrainStep:
         param_groups and the scheduler (one host sync); returns them."""
         return None if self.sched is None else self.sched.sync()
 
+    def release_scheduler(self):
+        """Sync and give the StepLR back to host control (its step() works
+        again); TrainStep then no longer steps it."""
+        if self.sched is None:
+            return None
+        lrs, self.sched = self.sched.release(), None
+        return lrs
+
     def __call__(self, label, feat):
         """One eager step; returns compute_loss's 8 outputs (device tensors)."""
+        if self.sched is not None:
+            self.sched.adopt_host_lr()
         if self.graph is not None:
             self.label.copy_(label)
             self.feat.copy_(feat)

@@ -164,3 +164,36 @@ def test_device_steplr_contract():
     assert d.sync() == [5e-4]
     assert opt.param_groups[0]["lr"] == 5e-4 and sched.last_epoch == 75
     assert sched.get_last_lr() == [5e-4]
+
+
+def test_device_steplr_keeps_host_objects_consistent():
+    """while TrainStep owns the StepLR, (1) opt.state_dict() and
+    sched.state_dict() carry the device lr / epoch (synced first), (2) a host
+    scheduler.step() raises instead of stepping twice, (3) a host edit of a
+    param group's lr is adopted by the device state (with a warning), and
+    release() hands the scheduler back (its step() works again)."""
+    import warnings
+
+    import mpvae_step
+    p = torch.nn.Parameter(torch.zeros(3))
+    opt = torch.optim.Adam([p], lr=1e-3, fused=True)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 2, 0.5)
+    d = mpvae_step.DeviceStepLR(sched, opt)
+    d.last_epoch.fill_(2)  # as if two applied updates decayed it on the device
+    d.lr.mul_(0.5)
+    assert opt.state_dict()["param_groups"][0]["lr"] == 5e-4
+    assert sched.state_dict()["last_epoch"] == 2 and opt.param_groups[0]["lr"] == 5e-4
+    with pytest.raises(RuntimeError, match="stepped on the device"):
+        sched.step()
+    opt.param_groups[0]["lr"] = 1e-2
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        d.adopt_host_lr()
+    assert d.lr.tolist() == [1e-2] and any("adopts" in str(x.message) for x in w)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        d.adopt_host_lr()  # unchanged since: nothing to adopt, no warning
+    assert not w
+    assert d.release() == [1e-2]
+    sched.step()  # host control again
+    assert sched.last_epoch == 3

@@ -14,6 +14,10 @@ and records the worst elements of d fe_out / d fx_out with the sample terms
 that dominate them (t under each arithmetic, E and 1 - E in fp32).
 
   python tools/c5_worst.py --seed 11 [--config c5|c4] > out.json
+  python tools/c5_worst.py --c4test 3 > out.json   (the inputs of
+      tests/test_gpu_parity.py::test_c4_full_size_against_fp64_reference, explicit
+      noise; adds the forward row statistics of the worst rows: the kernels'
+      rowstat against the reference's formulas on the kernels' own t)
 """
 import argparse
 import json
@@ -45,6 +49,21 @@ def inputs(cfg, seed):
     R = ((torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1)
          * (6.0 / (L + z)) ** 0.5)
     return (B, S, L, z, d), y, fe, fx, mus, R
+
+
+def c4test_inputs(seed):
+    """tests/test_gpu_parity.py::test_c4_full_size_against_fp64_reference's inputs."""
+    B, S, L, z, d = 512, 4096, 1024, 1024, 50
+    g = torch.Generator(device=DEV).manual_seed(1000 + seed)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    mus = [torch.randn((B, d), device=DEV, generator=g) * s for s in (1.0, 0.1, 1.0, 0.1)]
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * \
+        (6.0 / (L + z)) ** 0.5
+    noise = torch.randn((S, B, z), device=DEV, generator=g)
+    return (B, S, L, z, d), y, fe, fx, mus, R, noise
 
 
 def plane_noise(pl, B, S, z):
@@ -84,13 +103,20 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--config", default="c5", choices=sorted(CFG))
     ap.add_argument("--top", type=int, default=3)
+    ap.add_argument("--c4test", type=int, default=None)
     cli = ap.parse_args()
-    (B, S, L, z, d), y, fe, fx, mus, R = inputs(cli.config, cli.seed)
+    explicit = None
+    if cli.c4test is not None:
+        (B, S, L, z, d), y, fe, fx, mus, R, explicit = c4test_inputs(cli.c4test)
+        cli.config, cli.seed = "c4", cli.c4test
+    else:
+        (B, S, L, z, d), y, fe, fx, mus, R = inputs(cli.config, cli.seed)
     key = 55490 + cli.seed
     chunk = 64 if cli.config == "c5" else 256
     leaves = [x.clone().requires_grad_(True) for x in (fe, mus[0], mus[1], fx, mus[2], mus[3], R)]
     args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S, n_test_sample=S,
-                              mode="train", nll_coeff=0.1, c_coeff=200.0, mpvae_noise="philox",
+                              mode="train", nll_coeff=0.1, c_coeff=200.0,
+                              mpvae_noise="philox" if explicit is None else explicit,
                               mpvae_seed=key)
     out = mpvae.compute_loss(y, *leaves, args)
     out[0].backward()
@@ -100,11 +126,16 @@ def main():
     torch.cuda.empty_cache()
     be = HipShardBackend("f16x3")
     shape = be.shape(S, S, 0, B, L, z)
-    pl = be.make_noise(shape, DEV, key, 0)
-    noise = plane_noise(pl, B, S, z)
-    # the kernels' own t (the forward's T stash, (B, S, L) b-major)
+    if explicit is None:
+        pl = be.make_noise(shape, DEV, key, 0)
+        noise = plane_noise(pl, B, S, z)
+    else:
+        pl = be.prepare_noise(explicit, shape)
+        noise = lambda a, b: explicit[a:b]
+    # the kernels' own t (the forward's T stash, (B, S, L) b-major) and row statistics
     loc = be.forward_local(shape, y, fe, fx, be.prepare_R(R), pl, keep_T=True)
     T = loc["T"]
+    k_rowstat, k_bstat = loc["rowstat"].double(), loc["bstat"].double()
     del loc
     t_kern = lambda a, b: T[:, a:b, :L].permute(1, 0, 2)
     res = {"config": cli.config, "seed": cli.seed, "B": B, "S": S, "L": L, "z": z}
@@ -132,6 +163,15 @@ def main():
     refk = ChunkedElbo(y, fe, fx, R, noise, S, chunk=chunk, t_src=t_kern)
     refk.forward(*mus, 0.1, 200.0)
     rgk = refk.backward(0.1, 200.0, 1.0, None, None)
+    # the forward's row statistics (logp, P, N per branch) and per-row
+    # log-sum-exp terms: kernels against the reference on the same t
+    rs_diff = (k_rowstat - refk.rowstat).abs()
+    res["rowstat_max_abs_diff"] = {n: float(rs_diff[k].max()) for k, n in enumerate(
+        ("logp_e", "logp_x", "P_e", "N_e", "P_x", "N_x"))}
+    res["bstat_rel_diff"] = {n: float(((k_bstat[k] - (refk.m if k in (0, 2) else refk.Z)[k // 2]) /
+                                       (refk.m if k in (0, 2) else refk.Z)[k // 2]).abs().max())
+                             for k, n in ((0, "m_e"), (1, "Z_e"), (2, "m_x"), (3, "Z_x"))}
+    refk_rowstat, refk_m, refk_Z = refk.rowstat, refk.m, refk.Z
     del refk
     np_ = lambda t: t.detach().cpu().numpy()
     res["grad_err"] = {}
@@ -159,6 +199,18 @@ def main():
             gk, Ek = per_sample_terms(ref64, br, b, l, tkc)
             g32, E32 = per_sample_terms(ref64, br, b, l, t32c)
             dom = torch.topk((gk - g64).abs(), 3).indices.tolist()
+            # this row's softmax weights over s: kernels' statistics vs the
+            # reference's on the kernels' t (the forward's share of the error)
+            lp_k = k_rowstat[br, b]
+            w_k = torch.exp(lp_k - lp_k.max()) / torch.exp(lp_k - lp_k.max()).sum()
+            lp_r = refk_rowstat[br, b]
+            w_r = torch.exp(lp_r - refk_m[br, b]) / refk_Z[br, b]
+            top = torch.topk(w_r, 3).indices.tolist()
+            res.setdefault("rows", []).append({
+                "grad": "d" + k, "b": b, "max_abs_logp_diff": float((lp_k - lp_r).abs().max()),
+                "top_samples": [{"s": s_, "w_ref_on_kernel_t": float(w_r[s_]), "w_kernels": float(w_k[s_]),
+                                 "logp_ref_on_kernel_t": float(lp_r[s_]), "logp_kernels": float(lp_k[s_])}
+                                for s_ in top]})
             res["worst"].append({
                 "grad": "d" + k, "b": b, "l": l, "y": float(y[b, l]),
                 "rel_to_max": float(diff[b, l]) / scale_k,

@@ -3,10 +3,12 @@
 # 128-label forward tile and repeatability"): libmpvae_hip.so variants with
 # tools/race_study.patch applied and MPV_RACE bits set (bit 0: the 4-wave,
 # two-workgroups-per-CU 128 x 128 tile for 96 < L <= 128; the other bits: one
-# candidate fix each, see the patch), built here (`build`) and probed for
+# candidate fix each, see the patch; round 5 added 32768: drain every counter
+# and barrier at the K-loop exit, 65536: the stage copies by plain loads +
+# ds_write instead of LDS-DMA), built here (`build`) and probed for
 # bitwise repeatability on the GPU box (`run`).
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-VARIANTS="${VARIANTS:-0 1 3 5 9 17 33 69}"
+VARIANTS="${VARIANTS:-1 17 32769 65537}"
 case "$1" in
   build)
     cd "$R/mpvae-1_amd" && make -s >/dev/null || exit 1
