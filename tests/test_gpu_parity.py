@@ -391,7 +391,8 @@ def _assert_c45(errs, grad_rtol):
             e = errs[f"{k}_{mode}"]
             assert e <= grad_rtol, (k, mode, e)
         assert errs[f"{k}_ref_fp32"] <= grad_rtol, (k, errs[f"{k}_ref_fp32"])
-        peers = max(errs[f"{k}_ref_fp32"], errs[f"{k}_f32"], errs[f"{k}_ref_on_kernel_t"])
+        peers = max(errs[f"{k}_ref_fp32"], errs[f"{k}_f32"], errs[f"{k}_ref_on_kernel_t"],
+                    errs[f"{k}_ref_erf64_on_kernel_t"])
         assert errs[f"{k}_f16x3"] <= 2.0 * peers, (k, errs[f"{k}_f16x3"], peers)
     assert errs["t_kernels"] <= errs["t_fp32_gemm"], (errs["t_kernels"], errs["t_fp32_gemm"])
 
@@ -458,7 +459,8 @@ def test_c4_full_size_against_fp64_reference(seed, with_gI):
     rf, rg = run(ref)
     del ref
     rg_alt = {"ref_fp32": run(ref32)[1], "ref_erf64": run(mk(erf_fp64=True))[1],
-              "ref_on_kernel_t": run(mk(t_src=_t_source(T, L)))[1]}
+              "ref_on_kernel_t": run(mk(t_src=_t_source(T, L)))[1],
+              "ref_erf64_on_kernel_t": run(mk(t_src=_t_source(T, L), erf_fp64=True))[1]}
     del ref32, T
     torch.cuda.empty_cache()
     for gemm, (outs, grads) in got.items():
@@ -466,9 +468,9 @@ def test_c4_full_size_against_fp64_reference(seed, with_gI):
         errs.update({f"d{k}_{gemm}": rel_err(v, _np(rg[k])) for k, v in grads.items()})
     for tag, ga in rg_alt.items():
         errs.update({f"d{k}_{tag}": rel_err(_np(ga[k]), _np(rg[k])) for k in got["f16x3"][1]})
-    errs.update({f"d{k}_f16x3_vs_ref_on_kernel_t": rel_err(got["f16x3"][1][k],
-                                                            _np(rg_alt["ref_on_kernel_t"][k]))
-                 for k in got["f16x3"][1]})
+    for tag in ("ref_on_kernel_t", "ref_erf64_on_kernel_t"):
+        errs.update({f"d{k}_f16x3_vs_{tag}": rel_err(got["f16x3"][1][k], _np(rg_alt[tag][k]))
+                     for k in got["f16x3"][1]})
     record(f"c4_full_fp64ref_seed{seed}_{'with_gI' if with_gI else 'total_only'}", errs)
     for gemm in got:
         for k in OUTS:
@@ -534,7 +536,8 @@ def test_c5_full_size_against_fp64_reference(seed):
         errs.update({f"d{k}_{gemm}": rel_err(v, _np(rg[k])) for k, v in got[gemm].items()})
         if gemm == "f16x3":
             T = be.forward_local(shape, y, fe, fx, be.prepare_R(R), pl, keep_T=True)["T"]
-            alts = (("ref_fp32", dict(t_fp32=True)), ("ref_on_kernel_t", dict(t_src=_t_source(T, L))))
+            alts = (("ref_fp32", dict(t_fp32=True)), ("ref_on_kernel_t", dict(t_src=_t_source(T, L))),
+                    ("ref_erf64_on_kernel_t", dict(t_src=_t_source(T, L), erf_fp64=True)))
             errs.update(_t_accuracy(ref, mk(t_fp32=True), _t_source(T, L)))
             for tag, kw in alts:
                 alt = mk(**kw)
@@ -542,8 +545,8 @@ def test_c5_full_size_against_fp64_reference(seed):
                 ga = alt.backward(0.1, 200.0, 1.0, None, None)
                 del alt
                 errs.update({f"d{k}_{tag}": rel_err(_np(ga[k]), _np(rg[k])) for k in got[gemm]})
-                if tag == "ref_on_kernel_t":
-                    errs.update({f"d{k}_f16x3_vs_ref_on_kernel_t": rel_err(got[gemm][k], _np(ga[k]))
+                if tag.endswith("on_kernel_t"):
+                    errs.update({f"d{k}_f16x3_vs_{tag}": rel_err(got[gemm][k], _np(ga[k]))
                                  for k in got[gemm]})
             del T
         del ref, pl, noise  # noise holds a view of the 68.7 GB planes

@@ -28,13 +28,19 @@ INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
 KL_EPS, KL_WEIGHT = 1e-6, 1.1
 
 
-def probit_prob(u32, erf_fp64=False):
+def probit_prob(u32, erf_fp64=False, e_fp64=False):
     """E = Normal(0,1).cdf(u)(1-eps1) + eps1/2 in float32, op by op (oracle.probit_prob).
     erf_fp64: erf(x) evaluated in float64 and rounded once to float32 (a
     correctly rounded fp32 erf) in place of torch's fp32 erf -- the same
     formula with another legitimate fp32 erf, to measure what one-ulp
-    differences of E alone do to the gradients."""
+    differences of E alone do to the gradients.
+    e_fp64: the whole formula in float64 from the fp32 u (float64 result): the
+    model's own E, without the fp32 grid that 1 + erf(x) is rounded to (one
+    step of it is up to ~1 % of 1 - E where E is near 1, and of E near 0)."""
     d = u32.device
+    if e_fp64:
+        x = u32.to(F64) / math.sqrt(2.0)
+        return 0.5 * (1.0 + torch.erf(x)) * float(_C1) + float(_C0)
     x = u32 / _SQRT2.to(d)
     erf = torch.erf(x.to(F64)).to(F32) if erf_fp64 else torch.erf(x)
     cdf = 0.5 * (1.0 + erf)
@@ -54,7 +60,7 @@ class ChunkedElbo:
     forward and backward, and must return the same values)."""
 
     def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False, erf_fp64=False,
-                 t_src=None):
+                 t_src=None, e_fp64=False):
         self.y, self.fe, self.fx = y.to(F32), fe_out.to(F32), fx_out.to(F32)
         self.Rt = R.to(F32).to(F64).t().contiguous()          # R.T.float() (mpvae.py:165)
         self.noise, self.S, self.chunk = noise, int(S), int(chunk)
@@ -63,6 +69,8 @@ class ChunkedElbo:
         # measures how far fp32 arithmetic alone moves the results
         self.t_fp32 = bool(t_fp32)
         self.erf_fp64 = bool(erf_fp64)
+        # e_fp64: E in float64 (probit_prob) -- the model's exact E on the fp32 u
+        self.e_fp64 = bool(e_fp64)
         # t_src(s0, s1) -> (s1-s0, B, L) float32: t supplied from outside (e.g.
         # the product's own T stash) instead of computed here -- the
         # reference's formulas evaluated on another implementation's t, to
@@ -104,7 +112,7 @@ class ChunkedElbo:
         for s0, s1 in self._chunks():
             t, _ = self._t(s0, s1)
             for br, base in enumerate((self.fe, self.fx)):
-                E = probit_prob(t + base, self.erf_fp64)
+                E = probit_prob(t + base, self.erf_fp64, self.e_fp64)
                 logp, P, N, c = self._rows(E)
                 rows[br, :, s0:s1] = logp.t()
                 rows[2 + 2 * br, :, s0:s1] = P.t()
@@ -141,7 +149,7 @@ class ChunkedElbo:
             t, eps = self._t(s0, s1)
             G = None
             for br, (base, gind, out) in enumerate(((self.fe, g_IL, dfe), (self.fx, g_I, dfx))):
-                E = probit_prob(t + base, self.erf_fp64)
+                E = probit_prob(t + base, self.erf_fp64, self.e_fp64)
                 E = E.to(F64)
                 w = torch.exp(self.rowstat[br, :, s0:s1] - self.m[br][:, None]) / self.Z[br][:, None]
                 a = (-gn * w / B).t()[..., None]                    # (s, B, 1)

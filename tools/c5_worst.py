@@ -98,6 +98,35 @@ def per_sample_terms(ce, br, b, l, t_col):
     return gE * float(_C1) * INV_SQRT_2PI * torch.exp(-0.5 * u * u), E
 
 
+def flip_scan(y, base, t_row, d_obs, top=4):
+    """One sample row (b, s) of one branch: which labels' log q would move by
+    the observed logp difference d_obs if fl(erf(x)) -- the reference's first
+    rounding of E (x = u / sqrt 2 in fp32) -- were its fp32 neighbour instead,
+    and how close erf(x) lies to the midpoint between the two (|pos| = 0.5: a
+    tie; pos = erf(x) in fp64 minus torch's fp32 erf, in fp32 ulps of erf)."""
+    sq2 = torch.tensor(2.0 ** 0.5, dtype=F32, device=t_row.device)
+    u32 = t_row.to(F32) + base.to(F32)
+    x = u32 / sq2
+    e32 = torch.erf(x)
+    e64 = torch.erf(x.to(F64))
+    up = torch.nextafter(e32, torch.full_like(e32, 2.0))
+    dn = torch.nextafter(e32, torch.full_like(e32, -2.0))
+    yv = y.to(F64)
+
+    def logq(ev):
+        E = ((0.5 * (1.0 + ev)) * _C1.to(ev.device) + float(0.5e-6)).to(F64)
+        return yv * torch.log(E) + (1.0 - yv) * torch.log(1.0 - E)
+    l0 = logq(e32)
+    d_up, d_dn = logq(up) - l0, logq(dn) - l0
+    pos = (e64 - e32.to(F64)) / (up.to(F64) - e32.to(F64))
+    # the neighbour that reproduces d_obs best
+    d_best = torch.where((d_up - d_obs).abs() < (d_dn - d_obs).abs(), d_up, d_dn)
+    order = torch.topk(-(d_best - d_obs).abs(), top).indices.tolist()
+    return [{"l": l, "y": float(y[l]), "u": float(u32[l]), "E_ref": float(torch.exp(l0[l])) if y[l] == 1
+             else 1.0 - float(torch.exp(l0[l])), "dlogq_flip": float(d_best[l]),
+             "pos_ulps": float(pos[l])} for l in order]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seed", type=int, default=11)
@@ -206,10 +235,13 @@ def main():
             lp_r = refk_rowstat[br, b]
             w_r = torch.exp(lp_r - refk_m[br, b]) / refk_Z[br, b]
             top = torch.topk(w_r, 3).indices.tolist()
+            base_row = (fe if br == 0 else fx)[b, :L]
             res.setdefault("rows", []).append({
                 "grad": "d" + k, "b": b, "max_abs_logp_diff": float((lp_k - lp_r).abs().max()),
                 "top_samples": [{"s": s_, "w_ref_on_kernel_t": float(w_r[s_]), "w_kernels": float(w_k[s_]),
-                                 "logp_ref_on_kernel_t": float(lp_r[s_]), "logp_kernels": float(lp_k[s_])}
+                                 "logp_ref_on_kernel_t": float(lp_r[s_]), "logp_kernels": float(lp_k[s_]),
+                                 "flip_candidates": flip_scan(y[b, :L], base_row, T[b, s_, :L],
+                                                              float(lp_k[s_] - lp_r[s_]))}
                                 for s_ in top]})
             res["worst"].append({
                 "grad": "d" + k, "b": b, "l": l, "y": float(y[b, l]),
