@@ -372,28 +372,64 @@ def _t_source(T, L):
     return lambda a, b: T[:, a:b, :L].permute(1, 0, 2)
 
 
+# the reference's formulas on the kernels' own t (their T stash): with torch's
+# fp32 erf, with a correctly rounded one, and with the kernels' own erf and
+# argument rounding restated op by op (torch64_ref.kernel_probit_prob)
+ON_KERNEL_T = (("ref_on_kernel_t", {}), ("ref_erf64_on_kernel_t", dict(erf_fp64=True)),
+               ("ref_kerf_on_kernel_t", dict(kernel_erf=True)))
+
+
 def _assert_c45(errs, grad_rtol):
-    """The full-size gradient assertions, per case:
+    """The full-size gradient assertions, per case.
+
+    The yardstick is the reference's arithmetic with the exactly rounded t:
+    t the fp64 product of the fp32 operands rounded once, then u and E in fp32
+    op by op with torch's fp32 erf (tests/torch64_ref.py).  (E in fp64
+    instead puts every fp32 evaluation -- the reference's own, the kernels in
+    both modes -- 3.6e-3 (C4) and 1.2e-2 (C5) away, all alike: the fp32 grid
+    of 1 + erf near E = 1 is the reference's, not an error to measure.)
+    On that grid, erf(x) values near a rounding midpoint go either way in any
+    fp32 evaluation that rounds its argument or its erf differently: at C4
+    seed 3 the worst element (b 452, l 218) is one label-0 sample with erf(x)
+    1e-4 ulp from the midpoint; torch's fp32 erf rounds it one way, the
+    kernels' (argument fma(t, kZq, base kZq), erfc form) the other, which
+    moves log q by 7e-3 and the element by 6.8e-4 of the gradient's max
+    (tools/c5_worst.py --c4test 3, profiles/r05_c4_seed3_worst.json).  The
+    reference's formulas evaluated with the kernels' erf restated op by op
+    (ref_kerf_on_kernel_t) land on the same side: 6.82e-4, and 3.7e-6 from
+    the kernels.
+
+    Asserted per case:
       * every gradient within the stated absolute bound, and the reference's
         own fp32 spread under the same bound (the bound's premise);
-      * the f16x3 kernels within 2 x the largest of three fp32 evaluations
-        of the SAME inputs: the reference's arithmetic with t from an fp32
-        GEMM, the kernels in exact-fp32 MFMA mode, and the reference's
-        arithmetic on the kernels' own t (the T stash).  The last one is the
-        conditioning of this very t: at C5 seed 11 it reproduces the kernels'
-        3.6e-3 to four digits -- one label-0 element whose gradient is one
-        sample with E one fp32 ulp from 1 (profiles/r05_c5_seed11_worst.json);
+      * the f16x3 kernels within 2 x the largest of five fp32 evaluations of
+        the SAME inputs: the reference's arithmetic with t from an fp32 GEMM
+        (its tensordot), the kernels in exact-fp32 MFMA mode, and the
+        reference's arithmetic on the kernels' own t (their T stash) with
+        torch's erf, a correctly rounded erf, and the kernels' own fp32
+        erf (ON_KERNEL_T).
+        The on-kernel-t evaluations are the conditioning of this very t: at
+        C5 seed 11 they reproduce the kernels' 3.6e-3 to four digits -- one
+        label-0 element whose gradient is one sample with E one fp32 ulp from
+        1 (profiles/r05_c5_seed11_worst.json);
+      * the kernels within HEADLINE_GRAD_RTOL of the reference's formulas
+        evaluated with their own erf on their own t (ref_kerf_on_kernel_t):
+        what remains is rcp / exp2 last bits and summation order;
       * the kernels' t at least as accurate as an fp32 GEMM's (normwise max
         error against the fp64 product of the same operands), so that the
-        third evaluation is no licence for a worse t."""
+        on-kernel-t evaluations are no licence for a worse t."""
     for k in ("dfe_out", "dfx_out", "dr_sqrt_sigma"):
         for mode in ("f16x3", "f32"):
             e = errs[f"{k}_{mode}"]
             assert e <= grad_rtol, (k, mode, e)
         assert errs[f"{k}_ref_fp32"] <= grad_rtol, (k, errs[f"{k}_ref_fp32"])
-        peers = max(errs[f"{k}_ref_fp32"], errs[f"{k}_f32"], errs[f"{k}_ref_on_kernel_t"],
-                    errs[f"{k}_ref_erf64_on_kernel_t"])
+        peers = max(errs[f"{k}_{tag}"] for tag in ("ref_fp32", "f32") + tuple(t for t, _ in ON_KERNEL_T))
         assert errs[f"{k}_f16x3"] <= 2.0 * peers, (k, errs[f"{k}_f16x3"], peers)
+        # and the kernels are that restatement of their own arithmetic: the
+        # rest (hardware rcp / exp2 last bits, summation orders) within the
+        # headline gradient tolerance
+        e = errs[f"{k}_f16x3_vs_ref_kerf_on_kernel_t"]
+        assert e <= HEADLINE_GRAD_RTOL, (k, e)
     assert errs["t_kernels"] <= errs["t_fp32_gemm"], (errs["t_kernels"], errs["t_fp32_gemm"])
 
 
@@ -459,8 +495,7 @@ def test_c4_full_size_against_fp64_reference(seed, with_gI):
     rf, rg = run(ref)
     del ref
     rg_alt = {"ref_fp32": run(ref32)[1], "ref_erf64": run(mk(erf_fp64=True))[1],
-              "ref_on_kernel_t": run(mk(t_src=_t_source(T, L)))[1],
-              "ref_erf64_on_kernel_t": run(mk(t_src=_t_source(T, L), erf_fp64=True))[1]}
+              **{tag: run(mk(t_src=_t_source(T, L), **kw))[1] for tag, kw in ON_KERNEL_T}}
     del ref32, T
     torch.cuda.empty_cache()
     for gemm, (outs, grads) in got.items():
@@ -468,7 +503,7 @@ def test_c4_full_size_against_fp64_reference(seed, with_gI):
         errs.update({f"d{k}_{gemm}": rel_err(v, _np(rg[k])) for k, v in grads.items()})
     for tag, ga in rg_alt.items():
         errs.update({f"d{k}_{tag}": rel_err(_np(ga[k]), _np(rg[k])) for k in got["f16x3"][1]})
-    for tag in ("ref_on_kernel_t", "ref_erf64_on_kernel_t"):
+    for tag, _ in ON_KERNEL_T:
         errs.update({f"d{k}_f16x3_vs_{tag}": rel_err(got["f16x3"][1][k], _np(rg_alt[tag][k]))
                      for k in got["f16x3"][1]})
     record(f"c4_full_fp64ref_seed{seed}_{'with_gI' if with_gI else 'total_only'}", errs)
@@ -536,8 +571,8 @@ def test_c5_full_size_against_fp64_reference(seed):
         errs.update({f"d{k}_{gemm}": rel_err(v, _np(rg[k])) for k, v in got[gemm].items()})
         if gemm == "f16x3":
             T = be.forward_local(shape, y, fe, fx, be.prepare_R(R), pl, keep_T=True)["T"]
-            alts = (("ref_fp32", dict(t_fp32=True)), ("ref_on_kernel_t", dict(t_src=_t_source(T, L))),
-                    ("ref_erf64_on_kernel_t", dict(t_src=_t_source(T, L), erf_fp64=True)))
+            alts = (("ref_fp32", dict(t_fp32=True)),) + tuple(
+                (tag, dict(t_src=_t_source(T, L), **kw)) for tag, kw in ON_KERNEL_T)
             errs.update(_t_accuracy(ref, mk(t_fp32=True), _t_source(T, L)))
             for tag, kw in alts:
                 alt = mk(**kw)

@@ -80,3 +80,21 @@ def test_external_t_source_reproduces_own_t():
         ga, gb = own.backward(0.1, 200.0), ext.backward(0.1, 200.0)
         for k in ("fe_out", "fx_out", "r_sqrt_sigma"):
             assert torch.equal(ga[k], gb[k]), (kw, k)
+
+
+def test_kernel_erf_restatement_is_the_same_probit():
+    """kernel_probit_prob (the product's erf and argument rounding, both forms)
+    is the reference's E up to its fp32 rounding: the kernels round the
+    probit's argument differently (zq = fma(t, kZq, base kZq) instead of
+    u = t + base, then u / sqrt 2), which moves E by phi(u) times an ulp or two
+    of u (<= 5e-7 absolute, <= 5e-6 relative for 0.01 < E < 0.99)."""
+    from torch64_ref import kernel_probit_prob, probit_prob
+    g = torch.Generator().manual_seed(0)
+    t = torch.randn(200000, generator=g) * 1.2
+    base = torch.randn(200000, generator=g)
+    E = probit_prob(t + base).double()
+    for form in ("p", "q"):
+        Ek = kernel_probit_prob(t, base, form).double()
+        assert float((Ek - E).abs().max()) <= 5e-7
+        mid = (E > 0.01) & (E < 0.99)
+        assert float(((Ek - E).abs() / E)[mid].max()) <= 5e-6

@@ -28,23 +28,67 @@ INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
 KL_EPS, KL_WEIGHT = 1e-6, 1.1
 
 
-def probit_prob(u32, erf_fp64=False, e_fp64=False):
+def probit_prob(u32, erf_fp64=False):
     """E = Normal(0,1).cdf(u)(1-eps1) + eps1/2 in float32, op by op (oracle.probit_prob).
     erf_fp64: erf(x) evaluated in float64 and rounded once to float32 (a
     correctly rounded fp32 erf) in place of torch's fp32 erf -- the same
     formula with another legitimate fp32 erf, to measure what one-ulp
-    differences of E alone do to the gradients.
-    e_fp64: the whole formula in float64 from the fp32 u (float64 result): the
-    model's own E, without the fp32 grid that 1 + erf(x) is rounded to (one
-    step of it is up to ~1 % of 1 - E where E is near 1, and of E near 0)."""
+    differences of E alone do to the gradients."""
     d = u32.device
-    if e_fp64:
-        x = u32.to(F64) / math.sqrt(2.0)
-        return 0.5 * (1.0 + torch.erf(x)) * float(_C1) + float(_C0)
     x = u32 / _SQRT2.to(d)
     erf = torch.erf(x.to(F64)).to(F32) if erf_fp64 else torch.erf(x)
     cdf = 0.5 * (1.0 + erf)
     return cdf * _C1.to(d) + _C0.to(d)
+
+
+# The product's erf (mpvae-1_amd/csrc/mpv_common.h), restated op by op in fp32:
+# the same formula E = 0.5 (1 + erf(u / sqrt 2)) (1 - eps1) + eps1 / 2 with
+# erf = +-(1 - erfc(|z|)) from a Numerical-Recipes-form erfc, in the two forms
+# the kernels use -- "p" (forward: t exp2(P(t) - zq^2)) and "q" (element pass:
+# (t exp2(-zq^2)) Q(t)).  fp32 fmas are emulated in fp64 (exact product, then
+# rounded), the hardware reciprocal and exp2 as correctly rounded fp32 -- so
+# this is the kernels' erf up to those two instructions' last-bit error.
+def _f32(v):
+    import numpy as np
+    return float(np.float32(v))
+
+
+_KZQ = _f32(_f32(0.70710678118654752440) * _f32(1.2011224087864498))      # kZq
+_HALF_SQ = _f32(0.5 / _f32(1.2011224087864498))                            # 0.5f / kSqL2e
+_L2E = _f32(1.4426950408889634)
+_ERFC_P = [_f32(_f32(c) * _L2E) for c in (-0.139353514, 0.777093824, -1.58356997, 1.19629222,
+                                           -0.0702797193, 1.09342452, -1.27360696)]
+_ERFC_Q = [_f32(c) for c in (0.0899837102, -0.359859836, 0.38748431, 0.0453561664, 0.275197459,
+                             0.279788422, 0.282049996)]
+_KEH = _f32(0.5 * float(_C1))
+
+
+def _fma(a, b, c):
+    return (a.to(F64) * b + c).to(F32) if torch.is_tensor(b) else (a.to(F64) * float(b) + c).to(F32)
+
+
+def kernel_probit_prob(t32, base32, form):
+    """E of the kernels' arithmetic from t and fe/fx (fp32): zq = fma(t, kZq,
+    base kZq), w = 1 + erf through the form-p or form-q erfc, E = w kEh + C0
+    rounded twice (contract off), as probit_w2xN_zq / probit_dw2xN_zq and their
+    callers compute it."""
+    zq = _fma(t32, _KZQ, (base32.to(F64) * _KZQ).to(F32).to(F64))
+    den = _fma(zq.abs(), _HALF_SQ, 1.0)
+    t = (1.0 / den.to(F64)).to(F32).to(F64)
+    c = _ERFC_P if form == "p" else _ERFC_Q
+    p = _fma(t, c[0], c[1])
+    for ck in c[2:]:
+        p = _fma(t, p.to(F64), ck)
+    z64 = zq.to(F64)
+    if form == "p":
+        a = (-z64 * z64 + p.to(F64)).to(F32)
+        erfc = (t * torch.exp2(a.to(F64)).to(F32).to(F64)).to(F32)
+    else:
+        ez = torch.exp2((-z64 * z64).to(F32).to(F64)).to(F32)
+        erfc = ((t * ez.to(F64)).to(F32).to(F64) * p.to(F64)).to(F32)
+    om = (1.0 - erfc.to(F64)).to(F32)
+    w = (1.0 + torch.copysign(om, zq).to(F64)).to(F32)
+    return ((w.to(F64) * _KEH).to(F32).to(F64) + float(_C0)).to(F32)
 
 
 def label_sets(y):
@@ -60,7 +104,7 @@ class ChunkedElbo:
     forward and backward, and must return the same values)."""
 
     def __init__(self, y, fe_out, fx_out, R, noise, S, chunk=256, t_fp32=False, erf_fp64=False,
-                 t_src=None, e_fp64=False):
+                 t_src=None, kernel_erf=False):
         self.y, self.fe, self.fx = y.to(F32), fe_out.to(F32), fx_out.to(F32)
         self.Rt = R.to(F32).to(F64).t().contiguous()          # R.T.float() (mpvae.py:165)
         self.noise, self.S, self.chunk = noise, int(S), int(chunk)
@@ -69,8 +113,9 @@ class ChunkedElbo:
         # measures how far fp32 arithmetic alone moves the results
         self.t_fp32 = bool(t_fp32)
         self.erf_fp64 = bool(erf_fp64)
-        # e_fp64: E in float64 (probit_prob) -- the model's exact E on the fp32 u
-        self.e_fp64 = bool(e_fp64)
+        # kernel_erf: E by the product's own erf (kernel_probit_prob; form p in
+        # the forward, form q in the backward, as the kernels use them)
+        self.kernel_erf = bool(kernel_erf)
         # t_src(s0, s1) -> (s1-s0, B, L) float32: t supplied from outside (e.g.
         # the product's own T stash) instead of computed here -- the
         # reference's formulas evaluated on another implementation's t, to
@@ -94,6 +139,11 @@ class ChunkedElbo:
             return t.reshape(s1 - s0, B, -1), eps
         return (eps.to(F64).reshape(-1, z) @ self.Rt).reshape(s1 - s0, B, -1).to(F32), eps
 
+    def _E(self, t, base, form):
+        if self.kernel_erf:
+            return kernel_probit_prob(t, base.expand_as(t), form)
+        return probit_prob(t + base, self.erf_fp64)
+
     def _rows(self, E):
         E = E.to(F64)
         logp = (self.y64 * torch.log(E) + (1.0 - self.y64) * torch.log(1.0 - E)).sum(-1)
@@ -112,7 +162,7 @@ class ChunkedElbo:
         for s0, s1 in self._chunks():
             t, _ = self._t(s0, s1)
             for br, base in enumerate((self.fe, self.fx)):
-                E = probit_prob(t + base, self.erf_fp64, self.e_fp64)
+                E = self._E(t, base, "p")
                 logp, P, N, c = self._rows(E)
                 rows[br, :, s0:s1] = logp.t()
                 rows[2 + 2 * br, :, s0:s1] = P.t()
@@ -149,8 +199,7 @@ class ChunkedElbo:
             t, eps = self._t(s0, s1)
             G = None
             for br, (base, gind, out) in enumerate(((self.fe, g_IL, dfe), (self.fx, g_I, dfx))):
-                E = probit_prob(t + base, self.erf_fp64, self.e_fp64)
-                E = E.to(F64)
+                E = self._E(t, base, "q").to(F64)
                 w = torch.exp(self.rowstat[br, :, s0:s1] - self.m[br][:, None]) / self.Z[br][:, None]
                 a = (-gn * w / B).t()[..., None]                    # (s, B, 1)
                 bP = (scale[:, None] * self.rowstat[3 + 2 * br, :, s0:s1]).t()[..., None]
