@@ -496,6 +496,10 @@ struct Dr16Params {
 };
 
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
+#ifndef MPV_DR_FAST_DMA
+#define MPV_DR_FAST_DMA 1
+#endif
+constexpr bool kDrFastDma = MPV_DR_FAST_DMA;  // dR16s: DrsDma pointer walk
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -720,6 +724,48 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
   drs_issue_range<PER_WAVE, PIECES>(p, dst, q0, rows, wn * PER_WAVE, l0, z0, lane_u, lane_h);
 }
 
+// A group-0 wave's share of every stage's LDS-DMA: PER_WAVE consecutive rows
+// of one operand (the first WN/2 waves G rows, the others noise rows), walked
+// by 64-bit pointer increments -- two SALU per row instead of the ~14 of a
+// row * ld product and clamp per piece (drs_issue_range), which the wave
+// issued in the slot where the other group's MFMAs run.  Noise rows past the
+// last real row (a padded last stage) take the clamped per-piece path.
+template <int PER_WAVE, int PIECES, int WN>
+struct DrsDma {
+  const char* src;  // first row of this wave's share of the next stage
+  int64_t row_b;    // bytes per source row
+  int q, q_stage0;  // its row index; the stage's first row
+  int pc0;          // first piece (1-KB LDS row) of the share
+  bool is_g;
+  MPV_DEV void init(const Dr16Params& p, int q_first, int wn, int l0, int z0) {
+    static_assert(PIECES / 2 == (WN / 2) * PER_WAVE, "G rows on the first half of the waves");
+    static_assert(PER_WAVE % 8 == 0, "the source swizzle (row & 7) restarts with every share");
+    is_g = wn < WN / 2;
+    pc0 = wn * PER_WAVE;
+    q_stage0 = q_first;
+    q = q_first + (wn % (WN / 2)) * PER_WAVE;
+    row_b = is_g ? p.gld * 2 : p.eps16.ld * 2;
+    src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
+               : reinterpret_cast<const char*>(p.eps16.data + (int64_t)q * p.eps16.ld + 2 * z0);
+  }
+  MPV_DEV void issue(const Dr16Params& p, char* dst, int rows, int l0, int z0, int lane_u,
+                     int lane_h) {
+    if (is_g || q + PER_WAVE <= rows) {
+      const char* sp = src;
+#pragma unroll
+      for (int i = 0; i < PER_WAVE; ++i) {
+        lds_dma16(sp, (uint32_t)(((lane_u ^ (i & 7)) << 5) + lane_h), lds_addr(dst + (pc0 + i) * 1024));
+        sp += row_b;
+      }
+    } else {
+      drs_issue_range<PER_WAVE, PIECES>(p, dst, q_stage0, rows, pc0, l0, z0, lane_u, lane_h);
+    }
+    src += kDrKR * row_b;
+    q += kDrKR;
+    q_stage0 += kDrKR;
+  }
+};
+
 // Staggered schedule: the waves of row wm = 0 (group 0) and wm = 1 (group 1)
 // share the SIMDs pairwise and run one phase apart, so on every SIMD one wave
 // issues MFMAs while the other streams/reads.  Time is cut into slots ended by
@@ -776,15 +822,21 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   }
   barrier_raw();
   DrFrag<TM, TN> f;
+  DrsDma<PER_WAVE, PIECES, WN> dma;
+  if (kDrFastDma && grp == 0) dma.init(p, q_begin + kDrKR, wn, l0, z0);
   // the two groups run the same number of barriers: 2*nst + 1
   // (two stages per iteration, so that each image's LDS base is a constant
   // offset, spilled 84 VGPRs: 128 accumulator + 96 fragment VGPRs leave no room
   // for the hoisted addresses)
 #define DR_G0_STAGE(i, PAR)                                                                   \
   do {                                                                                        \
-    if ((i) + 1 < nst)                                                                        \
-      drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
-                                  rows, wn, l0, z0, lane_u, lane_h);                          \
+    if ((i) + 1 < nst) {                                                                      \
+      if (kDrFastDma)                                                                         \
+        dma.issue(p, smem + (1 - (PAR)) * STAGE, rows, l0, z0, lane_u, lane_h);               \
+      else                                                                                    \
+        drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
+                                    rows, wn, l0, z0, lane_u, lane_h);                        \
+    }                                                                                         \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
     lds_barrier();                                                                            \
     __builtin_amdgcn_s_setprio(1);                                                            \

@@ -13,21 +13,29 @@ step() {  # name, timeout, command...
   if [ $rc -ne 0 ]; then echo "[$n] rc=$rc"; tail -5 "$O/$n.err"; exit $rc; fi
   return 0
 }
-lib_of() { [ "$1" = new ] && echo "$R/mpvae-1_amd/libmpvae_hip.so" || echo "$R/abl/$1/libmpvae_hip.so"; }
+lib_of() {  # new: in-tree; a name with a slash: that directory; else abl/<name>
+  case "$1" in
+    new) echo "$R/mpvae-1_amd/libmpvae_hip.so" ;;
+    */*) echo "$R/$1/libmpvae_hip.so" ;;
+    *) echo "$R/abl/$1/libmpvae_hip.so" ;;
+  esac
+}
 for rep in ${REPS:-1 2}; do
   for v in $VARIANTS; do
+    vn=${v//\//_}
     for c in $CFGS; do
       g=--graph; [ "$c" = c4 ] || [ "$c" = c5 ] && g=
-      MPVAE_HIP_LIB=$(lib_of $v) step ${c}_${v}_$rep 300 python bench.py --config $c $g \
+      MPVAE_HIP_LIB=$(lib_of $v) step ${c}_${vn}_$rep 300 python bench.py --config $c $g \
         --steps ${STEPS:-50} --warmup 5 --no-cpu-baseline $BENCH_EXTRA
-      python -c "import json;d=json.load(open('$O/${c}_${v}_$rep.out'));print('$c $v',round(d['ms_per_step'],4),d['roofline']['ms_per_step_by_op'])"
+      python -c "import json;d=json.load(open('$O/${c}_${vn}_$rep.out'));print('$c $v',round(d['ms_per_step'],4),d['roofline']['ms_per_step_by_op'])"
     done
   done
 done
 if [ -n "$PROBE" ]; then
   for v in $VARIANTS; do
-    MPVAE_HIP_LIB=$(lib_of $v) PROBE_BWD=1 step probe_$v 300 python tools/repeat_probe.py $PROBE
-    cat "$O/probe_$v.out"
+    vn=${v//\//_}
+    MPVAE_HIP_LIB=$(lib_of $v) PROBE_BWD=1 step probe_$vn 300 python tools/repeat_probe.py $PROBE
+    cat "$O/probe_$vn.out"
   done
 fi
 echo done
