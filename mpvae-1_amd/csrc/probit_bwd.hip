@@ -500,6 +500,10 @@ constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
 #define MPV_DR_FAST_DMA 1
 #endif
 constexpr bool kDrFastDma = MPV_DR_FAST_DMA;  // dR16s: DrsDma pointer walk
+// timing study only (wrong results): group 0 does not wait for its stage DMA
+#ifndef MPV_DR_ABL_NOWAIT
+#define MPV_DR_ABL_NOWAIT 0
+#endif
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -724,6 +728,29 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
   drs_issue_range<PER_WAVE, PIECES>(p, dst, q0, rows, wn * PER_WAVE, l0, z0, lane_u, lane_h);
 }
 
+// Timing study (MPV_DR_STAMPS=1 builds only, tools/dr_stamps.py): s_memtime
+// at the slot boundaries of workgroup 0's waves over its first kDrStampStages
+// stages, stored by lane 0 with vector stores; read back through
+// mpv_study_dr_stamps.
+#ifndef MPV_DR_STAMPS
+#define MPV_DR_STAMPS 0
+#endif
+constexpr int kDrStampStages = 64, kDrStampPts = 6;
+#if MPV_DR_STAMPS
+__device__ unsigned long long mpv_dr_stamps[8][kDrStampStages][kDrStampPts];
+#define DR_STAMP(i, k)                                                                           \
+  do {                                                                                           \
+    if (blockIdx.x == 0 && (i) < kDrStampStages) {                                               \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                \
+      if (lane == 0) mpv_dr_stamps[wid][(i)][(k)] = t_;                                         \
+    }                                                                                            \
+  } while (0)
+#else
+#define DR_STAMP(i, k) \
+  do {                 \
+  } while (0)
+#endif
+
 // A group-0 wave's share of every stage's LDS-DMA: PER_WAVE consecutive rows
 // of one operand (the first WN/2 waves G rows, the others noise rows), walked
 // by 64-bit pointer increments -- two SALU per row instead of the ~14 of a
@@ -830,6 +857,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   // for the hoisted addresses)
 #define DR_G0_STAGE(i, PAR)                                                                   \
   do {                                                                                        \
+    DR_STAMP(i, 0);                                                                           \
     if ((i) + 1 < nst) {                                                                      \
       if (kDrFastDma)                                                                         \
         dma.issue(p, smem + (1 - (PAR)) * STAGE, rows, l0, z0, lane_u, lane_h);               \
@@ -837,22 +865,31 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
         drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
                                     rows, wn, l0, z0, lane_u, lane_h);                        \
     }                                                                                         \
+    DR_STAMP(i, 1);                                                                           \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
     lds_barrier();                                                                            \
+    DR_STAMP(i, 2);                                                                           \
     __builtin_amdgcn_s_setprio(1);                                                            \
     dr_mfma<TM, TN>(acc, f);                                                                  \
     __builtin_amdgcn_s_setprio(0);                                                            \
-    wait_vmcnt<0>();                                                                          \
+    DR_STAMP(i, 3);                                                                           \
+    if (!MPV_DR_ABL_NOWAIT) wait_vmcnt<0>();                                                  \
+    DR_STAMP(i, 4);                                                                           \
     barrier_raw();                                                                            \
+    DR_STAMP(i, 5);                                                                           \
   } while (0)
 #define DR_G1_STAGE(i, PAR)                                                      \
   do {                                                                           \
+    DR_STAMP(i, 0);                                                              \
     dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp); \
     lds_barrier();                                                               \
+    DR_STAMP(i, 2);                                                              \
     __builtin_amdgcn_s_setprio(1);                                               \
     dr_mfma<TM, TN>(acc, f);                                                     \
     __builtin_amdgcn_s_setprio(0);                                               \
+    DR_STAMP(i, 3);                                                              \
     barrier_raw();                                                               \
+    DR_STAMP(i, 5);                                                              \
   } while (0)
   if (grp == 0) {
     // slot 2i: stream stage i+1, read stage i; slot 2i+1: MFMAs of stage i
@@ -1288,4 +1325,11 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   return MPV_OK;
 }
 
+#if MPV_DR_STAMPS
+// study builds only: copy workgroup 0's slot stamps (8 x 64 x 6 u64) to host
+int mpv_study_dr_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mpv_dr_stamps), sizeof(mpv_dr_stamps), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 }  // extern "C"

@@ -6,11 +6,13 @@ n_sample Monte-Carlo draws.  The reference has no distributed code; what has
 to cross ranks for results identical to a single device (up to summation
 order) is:
 
-  forward   all_gather of the per-row log-sum-exp statistics bstat (6 x B floats:
-            local max m and sum Z of exp(logp - m) per branch + ranking sums),
-            combined exactly as M = max m_r, Z = sum Z_r exp(m_r - M)
-            (kernel mpv_bstat_combine); all_reduce(SUM) of the (2,B,L) sums of
-            E over s behind indiv_prob / indiv_prob_label.
+  forward   one all_reduce(SUM) of a packed buffer [the (2,B,L) sums of E over
+            s behind indiv_prob / indiv_prob_label | world slots of the per-row
+            log-sum-exp statistics bstat (6 x B floats: local max m and sum Z
+            of exp(logp - m) per branch + ranking sums)], each rank's bstat in
+            its own slot and zeros elsewhere, so the sum is also the exact
+            all_gather of bstat; combined as M = max m_r, Z = sum Z_r
+            exp(m_r - M) (kernel mpv_bstat_combine).
   backward  one all_reduce(SUM) of the packed [d fe_out | d fx_out | d r_sqrt_sigma]
             buffer (the local backward kernels write straight into it).
 
@@ -157,7 +159,22 @@ class SampleShardExchange:
                 + " -- seed torch and numpy identically on every rank (same batch, "
                   "dropout masks and reparameterisation draws)")
 
-    def combine(self, bstat, colsum, backend):
+    def stat_slots(self):
+        """(world, this rank's slot) of the packed forward statistics
+        (HipShardBackend.forward_local)."""
+        return self.world, dist.get_rank(self.group)
+
+    def combine(self, loc, backend):
+        """Global bstat and colsum from a shard's forward_local output: one
+        all_reduce of the packed [colsum | bstat slots] buffer (two collectives,
+        all_gather + all_reduce, for a backend that does not pack)."""
+        bstat, colsum, packed = loc["bstat"], loc["colsum"], loc.get("packed")
+        if packed is not None:
+            COMM_TIMER.run("combine_all_reduce", packed.device,
+                           lambda: dist.all_reduce(packed, group=self.group))
+            B = bstat.shape[1]
+            slots = packed[colsum.numel():].view(self.world, 6, B)
+            return backend.combine_bstats(slots), colsum
         parts = [torch.empty_like(bstat) for _ in range(self.world)]
         COMM_TIMER.run("combine_all_gather", bstat.device,
                        lambda: dist.all_gather(parts, bstat.contiguous(), group=self.group))

@@ -166,7 +166,12 @@ class HipShardBackend:
                                              H.stream_of(x32.device)), "mpv_convert")
         return out
 
-    def forward_local(self, shape, y, fe_out, fx_out, Rop, eps, keep_T):
+    def forward_local(self, shape, y, fe_out, fx_out, Rop, eps, keep_T, stat_slots=None):
+        """stat_slots = (world, slot): colsum and bstat are written into one
+        packed buffer [colsum (2 B L) | world slots of bstat (6 B)], this
+        shard's bstat into its slot and the other slots zero, so that ONE
+        all_reduce(SUM) of it both sums colsum and gathers bstat (x + 0 is
+        exact); returned as "packed" (SampleShardExchange.combine)."""
         lib = H.load_library()
         dev = y.device
         S, B, L = shape.S_local, shape.B, shape.L
@@ -174,8 +179,17 @@ class HipShardBackend:
         f32 = torch.float32
         T = self._buf((B, S, (L + 3) // 4 * 4), dev, f32) if keep_T else None
         rowstat = self._buf((6, B, S), dev, f32)
-        bstat = self._buf((6, B), dev, f32)
-        colsum = self._buf((2, B, L), dev, f32)
+        packed = None
+        if stat_slots is None:
+            bstat = self._buf((6, B), dev, f32)
+            colsum = self._buf((2, B, L), dev, f32)
+        else:
+            world, slot = stat_slots
+            n = 2 * B * L
+            packed = self._buf((n + world * 6 * B,), dev, f32)
+            packed[n:].zero_()
+            colsum = packed[:n].view(2, B, L)
+            bstat = packed[n + slot * 6 * B:n + (slot + 1) * 6 * B].view(6, B)
         nbytes = lib.mpv_fwd_workspace_bytes(shape)
         ws = self._buf((max(nbytes, 1),), dev, torch.uint8)
         if self.gemm == H.GEMM_F16X3:
@@ -185,7 +199,7 @@ class HipShardBackend:
         args = H.FwdArgs(H.ptr(y), H.ptr(fe_out), H.ptr(fx_out), self.gemm, *ops, H.ptr(T),
                          H.ptr(rowstat), H.ptr(bstat), H.ptr(colsum), H.ptr(ws), nbytes)
         H.check(lib.mpv_probit_fwd(shape, args, H.stream_of(dev)), "mpv_probit_fwd")
-        return dict(rowstat=rowstat, bstat=bstat, colsum=colsum, T=T)
+        return dict(rowstat=rowstat, bstat=bstat, colsum=colsum, T=T, packed=packed)
 
     def combine_bstats(self, gathered):
         R, _, B = gathered.shape
@@ -267,8 +281,11 @@ class LocalExchange:
     def verify_replicas(self, tensors):
         pass
 
-    def combine(self, bstat, colsum, backend):
-        return bstat, colsum
+    def stat_slots(self):
+        return None
+
+    def combine(self, loc, backend):
+        return loc["bstat"], loc["colsum"]
 
     def reduce_grads(self, flat):
         return flat
@@ -316,8 +333,9 @@ class ProbitELBO(torch.autograd.Function):
         Rop = be.prepare_R(R)
         need = ctx.needs_input_grad
         keep_T = need[1] or need[4] or need[7]
-        loc = be.forward_local(shape, y, fe_out, fx_out, Rop, eps, keep_T)
-        bstat, colsum = cfg.exchange.combine(loc["bstat"], loc["colsum"], be)
+        loc = be.forward_local(shape, y, fe_out, fx_out, Rop, eps, keep_T,
+                               stat_slots=cfg.exchange.stat_slots())
+        bstat, colsum = cfg.exchange.combine(loc, be)
         outs = be.finalize(shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
                            cfg.nll_coeff, cfg.c_coeff)
         ctx.set_materialize_grads(False)

@@ -40,11 +40,20 @@ class OracleShardBackend:
     def from_f32(self, x32, dtype):
         return x32.to(dtype)
 
-    def forward_local(self, shape, y, fe_out, fx_out, R32, eps, keep_T):
+    def forward_local(self, shape, y, fe_out, fx_out, R32, eps, keep_T, stat_slots=None):
         f = pe.shard_forward(y.numpy(), fe_out.detach().numpy(), fx_out.detach().numpy(),
                              R32.numpy(), eps.numpy())
-        return dict(rowstat=_t(f["rowstat"]), bstat=_t(f["bstat"]), colsum=_t(f["colsum"]),
-                    T=f if keep_T else None)
+        out = dict(rowstat=_t(f["rowstat"]), bstat=_t(f["bstat"]), colsum=_t(f["colsum"]),
+                   T=f if keep_T else None, packed=None)
+        if stat_slots is not None:  # the product's packed layout (HipShardBackend)
+            world, slot = stat_slots
+            n, m = out["colsum"].numel(), out["bstat"].numel()
+            packed = torch.zeros(n + world * m, dtype=torch.float32)
+            packed[:n] = out["colsum"].reshape(-1)
+            packed[n + slot * m:n + (slot + 1) * m] = out["bstat"].reshape(-1)
+            out.update(packed=packed, colsum=packed[:n].view(out["colsum"].shape),
+                       bstat=packed[n + slot * m:n + (slot + 1) * m].view(out["bstat"].shape))
+        return out
 
     def combine_bstats(self, gathered):
         return _t(pe.combine_bstats(list(gathered.double().numpy())))

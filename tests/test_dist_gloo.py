@@ -199,6 +199,8 @@ def test_comm_timer_records_every_collective():
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, summ in results:
-        assert set(summ) == {"combine_all_gather", "combine_all_reduce", "reduce_grads"}, summ
+        # the forward's statistics travel in one packed all_reduce
+        assert set(summ) == {"combine_all_reduce", "reduce_grads"}, summ
+        assert all(d["calls"] in (None, 2) for d in summ.values()), summ
         for op, d in summ.items():
             assert d["device_ms"] is None and d["host_ms"] > 0.0, (rank, op, d)
