@@ -496,14 +496,6 @@ struct Dr16Params {
 };
 
 constexpr int kDrKR = 32;     // K rows per stage (one MFMA k-step)
-#ifndef MPV_DR_FAST_DMA
-#define MPV_DR_FAST_DMA 1
-#endif
-constexpr bool kDrFastDma = MPV_DR_FAST_DMA;  // dR16s: DrsDma pointer walk
-// timing study only (wrong results): group 0 does not wait for its stage DMA
-#ifndef MPV_DR_ABL_NOWAIT
-#define MPV_DR_ABL_NOWAIT 0
-#endif
 
 MPV_DEV s16x4 tr_read(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -687,6 +679,56 @@ MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0
   }
 }
 
+// dr_read with a group-0 wave's share of the next stage's LDS-DMA woven in:
+// one or two 1-KB pieces after each tile's four transposed reads, so the
+// CU's load path (the DMA) and the LDS (the reads) work side by side instead
+// of the reads queueing behind the whole DMA burst (tools/dr_stamps.py: DMA
+// issue 1060 + reads 960 ticks, serial, against 1650 for the other group's
+// MFMAs).  Noise rows past the last real one (a padded last stage) repeat
+// that row, as drs_issue_range clamps them.
+template <int TM, int TN, int ROWB, int IMG, int PER_WAVE, class Dma>
+MPV_DEV void dr_read_dma(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0, int r1,
+                         int sw, int tp, Dma& dma, char* dst, int rows, int lane_u, int lane_h) {
+  constexpr int STEPS = TM + TN;
+  // the per-piece source swizzle is recomputed next to its DMA, not hoisted
+  // out of the stage loop (8 more live VGPRs spill the accumulators)
+  int lu = lane_u;
+  asm volatile("" : "+v"(lu));
+  const char* sp = dma.src;
+  int nvalid = PER_WAVE;
+  if (!dma.is_g) {
+    const int over = dma.q - (rows - 1);
+    if (over > 0) sp -= over * dma.row_b;
+    nvalid = max(1, min(PER_WAVE, rows - dma.q));
+  }
+#pragma unroll
+  for (int k = 0; k < STEPS; ++k) {
+    const bool is_a = k < TM;
+    const int t = is_a ? wm * TM + k : wn * TN + (k - TM), uh = (t >> 1) * 4 + (t & 1);
+    const int ch = ((uh ^ sw) << 5) + tp * 8, cl = (((uh + 2) ^ sw) << 5) + tp * 8;
+    const char* img = is_a ? base : base + IMG;
+    const s16x8 hi = __builtin_shufflevector(tr_read(img, r0 * ROWB + ch), tr_read(img, r1 * ROWB + ch),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+    const s16x8 lo = __builtin_shufflevector(tr_read(img, r0 * ROWB + cl), tr_read(img, r1 * ROWB + cl),
+                                             0, 1, 2, 3, 4, 5, 6, 7);
+    if (is_a) {
+      f.ah[k] = hi;
+      f.al[k] = lo;
+    } else {
+      f.bh[k - TM] = hi;
+      f.bl[k - TM] = lo;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = k * PER_WAVE / STEPS; i < (k + 1) * PER_WAVE / STEPS; ++i) {
+      lds_dma16(sp, (uint32_t)(((lu ^ (i & 7)) << 5) + lane_h), lds_addr(dst + (dma.pc0 + i) * 1024));
+      sp += (i + 1 < nvalid) ? dma.row_b : 0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  dma.end();
+}
+
 template <int TM, int TN>
 MPV_DEV void dr_mfma(f32x4 (&acc)[TM][TN], const DrFrag<TM, TN>& f) {
 #pragma unroll
@@ -721,13 +763,6 @@ MPV_DEV void drs_issue_range(const Dr16Params& p, char* dst, int q0, int rows, i
   }
 }
 
-// One stage's LDS-DMA for wave wn of group 0: pieces wn*PER_WAVE ...
-template <int PER_WAVE, int PIECES>
-MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn, int l0, int z0,
-                       int lane_u, int lane_h) {
-  drs_issue_range<PER_WAVE, PIECES>(p, dst, q0, rows, wn * PER_WAVE, l0, z0, lane_u, lane_h);
-}
-
 // Timing study (MPV_DR_STAMPS=1 builds only, tools/dr_stamps.py): s_memtime
 // at the slot boundaries of workgroup 0's waves over its first kDrStampStages
 // stages, stored by lane 0 with vector stores; read back through
@@ -735,7 +770,7 @@ MPV_DEV void drs_issue(const Dr16Params& p, char* dst, int q0, int rows, int wn,
 #ifndef MPV_DR_STAMPS
 #define MPV_DR_STAMPS 0
 #endif
-constexpr int kDrStampStages = 64, kDrStampPts = 6;
+[[maybe_unused]] constexpr int kDrStampStages = 64, kDrStampPts = 6;
 #if MPV_DR_STAMPS
 __device__ unsigned long long mpv_dr_stamps[8][kDrStampStages][kDrStampPts];
 #define DR_STAMP(i, k)                                                                           \
@@ -754,42 +789,29 @@ __device__ unsigned long long mpv_dr_stamps[8][kDrStampStages][kDrStampPts];
 // A group-0 wave's share of every stage's LDS-DMA: PER_WAVE consecutive rows
 // of one operand (the first WN/2 waves G rows, the others noise rows), walked
 // by 64-bit pointer increments -- two SALU per row instead of the ~14 of a
-// row * ld product and clamp per piece (drs_issue_range), which the wave
-// issued in the slot where the other group's MFMAs run.  Noise rows past the
-// last real row (a padded last stage) take the clamped per-piece path.
+// row * ld product and clamp per piece (round 5: the stage's DMA block 325 ->
+// 139 instructions, dR -1.5 %, profiles/r05_dr_dma_ab.json).
 template <int PER_WAVE, int PIECES, int WN>
 struct DrsDma {
   const char* src;  // first row of this wave's share of the next stage
   int64_t row_b;    // bytes per source row
-  int q, q_stage0;  // its row index; the stage's first row
+  int q;            // its row index
   int pc0;          // first piece (1-KB LDS row) of the share
   bool is_g;
   MPV_DEV void init(const Dr16Params& p, int q_first, int wn, int l0, int z0) {
     static_assert(PIECES / 2 == (WN / 2) * PER_WAVE, "G rows on the first half of the waves");
     static_assert(PER_WAVE % 8 == 0, "the source swizzle (row & 7) restarts with every share");
-    is_g = wn < WN / 2;
-    pc0 = wn * PER_WAVE;
-    q_stage0 = q_first;
-    q = q_first + (wn % (WN / 2)) * PER_WAVE;
+    const int pc = wn * PER_WAVE;
+    is_g = pc < PIECES / 2;
+    pc0 = pc;
+    q = q_first + (is_g ? pc : pc - PIECES / 2);
     row_b = is_g ? p.gld * 2 : p.eps16.ld * 2;
     src = is_g ? reinterpret_cast<const char*>(p.g + (int64_t)q * p.gld + 2 * l0)
                : reinterpret_cast<const char*>(p.eps16.data + (int64_t)q * p.eps16.ld + 2 * z0);
   }
-  MPV_DEV void issue(const Dr16Params& p, char* dst, int rows, int l0, int z0, int lane_u,
-                     int lane_h) {
-    if (is_g || q + PER_WAVE <= rows) {
-      const char* sp = src;
-#pragma unroll
-      for (int i = 0; i < PER_WAVE; ++i) {
-        lds_dma16(sp, (uint32_t)(((lane_u ^ (i & 7)) << 5) + lane_h), lds_addr(dst + (pc0 + i) * 1024));
-        sp += row_b;
-      }
-    } else {
-      drs_issue_range<PER_WAVE, PIECES>(p, dst, q_stage0, rows, pc0, l0, z0, lane_u, lane_h);
-    }
+  MPV_DEV void end() {  // on to the next stage
     src += kDrKR * row_b;
     q += kDrKR;
-    q_stage0 += kDrKR;
   }
 };
 
@@ -798,11 +820,17 @@ struct DrsDma {
 // issues MFMAs while the other streams/reads.  Time is cut into slots ended by
 // one barrier each; group 0 does mem(i) in slot 2i and mma(i) in slot 2i+1,
 // group 1 does mem(i) in slot 2i+1 and mma(i) in slot 2i+2.
-//   mem(i): [group 0 only: LDS-DMA stage i+1 into image (i+1)%2 -- read by
-//           group 1 in slot 2i-1, so free] + fragment reads of stage i.
+//   mem(i): fragment reads of stage i; group 0 weaves the LDS-DMA of stage i+1
+//           into image (i+1)%2 (read by group 1 in slot 2i-1, so free) into
+//           them (dr_read_dma).
 //   mma(i): 96 MFMAs; group 0 then waits for its stage i+1 DMA, so stage i+1
 //           is visible to both groups after the slot's barrier.
-// Two 64-KB stage images; DMA latency budget = one slot pair.
+// Two 64-KB stage images; DMA latency budget = one slot pair.  Round 5
+// (tools/dr_stamps.py, profiles/r05_dr_ab.json): with the DMA as a burst ahead
+// of the reads, group 0's mem slot (1060 + 960 ticks) outlasted the other
+// group's MFMAs (1650) every slot; woven, dR -4.2 %.  Measured slower: group 1
+// issuing the stream between its own MFMAs (+2.3 %), and half of it in each
+// group's read slot (+12 %).
 template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   static_assert(WM == 2, "two wave groups");
@@ -847,62 +875,56 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
                                          lane_h);
     wait_vmcnt<0>();
   }
-  barrier_raw();
   DrFrag<TM, TN> f;
   DrsDma<PER_WAVE, PIECES, WN> dma;
-  if (kDrFastDma && grp == 0) dma.init(p, q_begin + kDrKR, wn, l0, z0);
+  if (grp == 0) dma.init(p, q_begin + kDrKR, wn, l0, z0);
+  barrier_raw();
   // the two groups run the same number of barriers: 2*nst + 1
-  // (two stages per iteration, so that each image's LDS base is a constant
-  // offset, spilled 84 VGPRs: 128 accumulator + 96 fragment VGPRs leave no room
-  // for the hoisted addresses)
-#define DR_G0_STAGE(i, PAR)                                                                   \
-  do {                                                                                        \
-    DR_STAMP(i, 0);                                                                           \
-    if ((i) + 1 < nst) {                                                                      \
-      if (kDrFastDma)                                                                         \
-        dma.issue(p, smem + (1 - (PAR)) * STAGE, rows, l0, z0, lane_u, lane_h);               \
-      else                                                                                    \
-        drs_issue<PER_WAVE, PIECES>(p, smem + (1 - (PAR)) * STAGE, q_begin + ((i) + 1) * kDrKR, \
-                                    rows, wn, l0, z0, lane_u, lane_h);                        \
-    }                                                                                         \
-    DR_STAMP(i, 1);                                                                           \
-    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp);              \
-    lds_barrier();                                                                            \
-    DR_STAMP(i, 2);                                                                           \
-    __builtin_amdgcn_s_setprio(1);                                                            \
-    dr_mfma<TM, TN>(acc, f);                                                                  \
-    __builtin_amdgcn_s_setprio(0);                                                            \
-    DR_STAMP(i, 3);                                                                           \
-    if (!MPV_DR_ABL_NOWAIT) wait_vmcnt<0>();                                                  \
-    DR_STAMP(i, 4);                                                                           \
-    barrier_raw();                                                                            \
-    DR_STAMP(i, 5);                                                                           \
-  } while (0)
-#define DR_G1_STAGE(i, PAR)                                                      \
-  do {                                                                           \
-    DR_STAMP(i, 0);                                                              \
-    dr_read<TM, TN, ROWB, IMG>(f, smem + (PAR) * STAGE, wm, wn, r0, r1, sw, tp); \
-    lds_barrier();                                                               \
-    DR_STAMP(i, 2);                                                              \
-    __builtin_amdgcn_s_setprio(1);                                               \
-    dr_mfma<TM, TN>(acc, f);                                                     \
-    __builtin_amdgcn_s_setprio(0);                                               \
-    DR_STAMP(i, 3);                                                              \
-    barrier_raw();                                                               \
-    DR_STAMP(i, 5);                                                              \
-  } while (0)
   if (grp == 0) {
-    // slot 2i: stream stage i+1, read stage i; slot 2i+1: MFMAs of stage i
-    // (stage i+1 landed before its barrier)
-    for (int i = 0; i < nst; ++i) DR_G0_STAGE(i, i & 1);
+    // slot 2i: read stage i with stage i+1's DMA woven in; slot 2i+1: MFMAs
+    // of stage i, then stage i+1 landed before the closing barrier
+    int i = 0;
+    for (; i + 1 < nst; ++i) {
+      DR_STAMP(i, 0);
+      dr_read_dma<TM, TN, ROWB, IMG, PER_WAVE>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp,
+                                               dma, smem + (1 - (i & 1)) * STAGE, rows, lane_u,
+                                               lane_h);
+      lds_barrier();
+      DR_STAMP(i, 2);
+      __builtin_amdgcn_s_setprio(1);
+      dr_mfma<TM, TN>(acc, f);
+      __builtin_amdgcn_s_setprio(0);
+      DR_STAMP(i, 3);
+      wait_vmcnt<0>();
+      DR_STAMP(i, 4);
+      barrier_raw();
+      DR_STAMP(i, 5);
+    }
+    for (; i < nst; ++i) {  // the last stage: nothing to stream
+      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
+      lds_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      dr_mfma<TM, TN>(acc, f);
+      __builtin_amdgcn_s_setprio(0);
+      barrier_raw();
+    }
     barrier_raw();
   } else {
     barrier_raw();
     // slot 2i+1: read stage i; slot 2i+2: MFMAs of stage i
-    for (int i = 0; i < nst; ++i) DR_G1_STAGE(i, i & 1);
+    for (int i = 0; i < nst; ++i) {
+      DR_STAMP(i, 0);
+      dr_read<TM, TN, ROWB, IMG>(f, smem + (i & 1) * STAGE, wm, wn, r0, r1, sw, tp);
+      lds_barrier();
+      DR_STAMP(i, 2);
+      __builtin_amdgcn_s_setprio(1);
+      dr_mfma<TM, TN>(acc, f);
+      __builtin_amdgcn_s_setprio(0);
+      DR_STAMP(i, 3);
+      barrier_raw();
+      DR_STAMP(i, 5);
+    }
   }
-#undef DR_G0_STAGE
-#undef DR_G1_STAGE
   const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
 #pragma unroll
   for (int m = 0; m < TM; ++m)
