@@ -50,6 +50,6 @@ for e in prof.key_averages():
         rows.append({"op": e.key, "calls_per_step": e.count / cli.steps,
                      "device_us_per_step": dt / cli.steps})
 rows.sort(key=lambda r: -r["device_us_per_step"])
-print(json.dumps({"n_sample": cli.n_sample, "dist": cli.dist, "ops": rows[:60]}, indent=1))
+print(json.dumps({"n_sample": cli.n_sample, "dist": cli.dist, "ops": rows[:60]}, indent=1), flush=True)
 if cli.dist:
     dist.destroy_process_group()
