@@ -829,8 +829,9 @@ struct DrsDma {
 // (tools/dr_stamps.py, profiles/r05_dr_ab.json): with the DMA as a burst ahead
 // of the reads, group 0's mem slot (1060 + 960 ticks) outlasted the other
 // group's MFMAs (1650) every slot; woven, dR -4.2 %.  Measured slower: group 1
-// issuing the stream between its own MFMAs (+2.3 %), and half of it in each
-// group's read slot (+12 %).
+// issuing the stream between its own MFMAs (+2.3 %), half of it in each
+// group's read slot (+12 % woven, +0.8 % with group 1's half ahead of its
+// reads).
 template <int WM, int WN, int TM, int TN>
 __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
   static_assert(WM == 2, "two wave groups");
