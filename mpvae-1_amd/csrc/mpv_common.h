@@ -163,6 +163,7 @@ MPV_DEV void probit_eval2xN(const f32x2 (&u)[N], f32x2 (&E)[N], f32x2 (&phi)[N])
 // 1 + erf is exact for u < 0 (Sterbenz), so a small E keeps its relative
 // precision; folding a rounded 0.5 C1 + C0 into one constant would not.
 constexpr float kEh = 0.5f * kC1;
+constexpr float kPhiK = kC1 * kInvSqrt2Pi;  // dE/du = kPhiK exp(-u^2/2)
 //
 // P(t) here is a degree-6 minimax fit of log(erfc(z) / t) + z^2 over
 // t >= 0.38 (|u| <= 4.6; tools/fit_erfc.py) in place of the degree-9
@@ -217,15 +218,17 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
   for (int j = 0; j < N; ++j) E[j] = pk_fma(E[j], splat2(kEh), splat2(kC0));
 }
 
-// probit_w2xN_zq for the backward: w (E = kEh w + C0) and phic =
-// (1 - 1e-6) phi(u), the factor dE/du needs.  exp(-z^2) gives phi, so erfc
+// probit_w2xN_zq for the backward: w (E = kEh w + C0) and ez = exp(-u^2/2),
+// which times kPhiK = (1 - 1e-6)/sqrt(2 pi) is the factor dE/du needs (the
+// element pass folds kPhiK into its row and column coefficients, so the
+// product is one multiply per element, not two).  exp(-z^2) gives phi, so erfc
 // is taken as t exp(-z^2) Q(t) with Q a degree-6 minimax fit of
 // erfcx(z) / t over t >= 0.38 (relative; tools/fit_erfc.py, form q) instead
 // of a second exponential of P(t).  fp32-emulated E error over |u| <= 40:
 // max 2.4e-6 (the forward's P form 2.6e-6, NR 2.46e-6).
 constexpr int kErfcxDeg = 6;
 template <int N>
-MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&phic)[N]) {
+MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&ezo)[N]) {
 #pragma clang fp contract(off)
   constexpr float c[kErfcxDeg + 1] = {0.0899837102f, -0.359859836f, 0.38748431f,
                                       0.0453561664f, 0.275197459f,  0.279788422f,
@@ -246,7 +249,7 @@ MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&phic)[
   for (int j = 0; j < N; ++j) {
     const f32x2 az = -zq[j] * zq[j];
     const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
-    phic[j] = ez * (kC1 * kInvSqrt2Pi);
+    ezo[j] = ez;
     const f32x2 om = splat2(1.0f) - (t[j] * ez) * q[j];
     w[j] = splat2(1.0f) +
            f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};

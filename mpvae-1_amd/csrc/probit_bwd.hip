@@ -88,9 +88,11 @@ __global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
       float bN = nrm > 0.0f ? cs * P : 0.0f;
       bmax = fmaxf(bmax, kBoundDl * fabsf(alpha) + kBoundPos * fabsf(bP) + kBoundNeg * fabsf(bN));
       if (dead) alpha = bP = bN = __builtin_nanf("");
-      coef[((int64_t)(3 * br + 0) * B + b) * S + s] = alpha;
-      coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP;
-      coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN;
+      // stored times dE/du's constant kPhiK (the element pass then multiplies
+      // by exp(-u^2/2) alone)
+      coef[((int64_t)(3 * br + 0) * B + b) * S + s] = alpha * kPhiK;
+      coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP * kPhiK;
+      coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN * kPhiK;
     }
     bmaxb[br] = bmax;
   }
@@ -126,12 +128,14 @@ struct ElemParams {
 // Per-column constants of the element pass (the lane's four label columns).
 struct ElemCol {
   f32x2 base[4];  // fe_out, fx_out, in the probit's argument units (x kZq)
-  f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total
+  f32x2 gind[4];  // g(indiv_prob_label), g(indiv_prob), / S_total, x kPhiK
   float y[4];
   bool soft[4];
   float qm[4];  // d = E + qm: E - 1 for y = 0 (the sign of d logp/dE folded in), E otherwise
   float sga[4];   // e^{-5E} (y = 1) or e^{5E} as exp2(sga w) e^{-+5 C0}
   float wp[4], wn[4];  // [y = 1], [y = 0]
+  bool pos[4];         // y = 1
+  float kp, kn;        // e^{-5 C0}, e^{5 C0} (the nonzero wp, wn)
 };
 
 // Four elements (columns) of one row at once, step-major so that the
@@ -145,11 +149,14 @@ struct ElemCol {
 template <bool SOFT = true, bool NANCHK = true, bool SOFT_RCP = false>
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
                        f32x2 (&out)[4]) {
-  f32x2 zq[4], w[4], phic[4];
+  f32x2 zq[4], w[4], ez[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) zq[q] = pk_fma(splat2(t[q]), splat2(kZq), c.base[q]);
-  probit_dw2xN_zq<4>(zq, w, phic);
+  probit_dw2xN_zq<4>(zq, w, ez);
   const f32x2 nbP = -bP;
+  // the ranking coefficient of a positive / negative label of this row (a
+  // binary block picks one per column instead of forming wn bN + wp (-bP))
+  const f32x2 rkp = splat2(c.kp) * nbP, rkn = splat2(c.kn) * bN;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // E in the reference's rounding order (mpvae.py:171-180: cdf = 0.5 (1 +
@@ -178,10 +185,11 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
       dE = pk_fma(alpha, r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-    const f32x2 rk = pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP);
+    const f32x2 rk = SOFT ? pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP)
+                          : (c.pos[q] ? rkp : rkn);
     const f32x2 a = w[q] * c.sga[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
-    out[q] = dE * phic[q];
+    out[q] = dE * ez[q];  // the coefficients carry kPhiK
   }
   // a degenerate row poisons every label, whatever its value (reference autograd)
   if (NANCHK && (bP.x != bP.x || bP.y != bP.y)) {
@@ -224,6 +232,8 @@ MPV_DEV void elem_row_load(ElemRow& r, const ElemParams& p, int b, int s, int c0
 MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, bool (&ok)[4],
                             ElemCol& ec) {
   const int L = p.L;
+  ec.kp = exp2f((-5.0f * 1.4426950408889634f) * kC0);
+  ec.kn = exp2f((5.0f * 1.4426950408889634f) * kC0);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = c0 + q;
@@ -235,15 +245,16 @@ MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, boo
     const float gi = (ok[q] && p.gI) ? p.gI[o] * p.inv_S : 0.0f;
     const float gil = (ok[q] && p.gIL) ? p.gIL[o] * p.inv_S : 0.0f;
     ec.base[q] = f32x2{fe, fx} * kZq;
-    ec.gind[q] = f32x2{gil, gi};
+    ec.gind[q] = f32x2{gil, gi} * kPhiK;
     ec.y[q] = yv;
     ec.soft[q] = !(yv == 0.0f || yv == 1.0f);
     ec.qm[q] = yv == 0.0f ? -1.0f : 0.0f;  // E - 1 = -(1 - E), or E
     const float sgx = (yv == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
     ec.sga[q] = sgx * kEh;
     // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
-    ec.wp[q] = yv == 1.0f ? exp2f(sgx * kC0) : 0.0f;
-    ec.wn[q] = yv == 0.0f ? exp2f(sgx * kC0) : 0.0f;
+    ec.wp[q] = yv == 1.0f ? ec.kp : 0.0f;
+    ec.wn[q] = yv == 0.0f ? ec.kn : 0.0f;
+    ec.pos[q] = yv == 1.0f;
   }
 }
 
