@@ -428,6 +428,34 @@ MPV_DEV void split_f16(float x, float s, uint16_t& hi, uint16_t& lo) {
   lo = __builtin_bit_cast(uint16_t, l);
 }
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// split_f16 of two values at once, x0 in bits 0-15 and x1 in bits 16-31 of
+// the hi and lo words, bit for bit: v_fma_mix rounds fma(s, x, -0) = x*s
+// (exact: s is a power of two; the -0 addend keeps a -0's sign) and then
+// fma(s, x, -hi) = x*s - hi (exact in fp32) once to fp16, four instructions
+// where the plain form takes a multiply, a convert, a convert back and a
+// subtract per value.
+MPV_DEV void split2_f16(float x0, float x1, float s, uint32_t& hi, uint32_t& lo) {
+  const float nz = -0.0f;
+  uint32_t h, l;
+  asm("v_fma_mixlo_f16 %0, %2, %3, %5\n\t"
+      "v_fma_mixhi_f16 %0, %2, %4, %5\n\t"
+      "v_fma_mixlo_f16 %1, %2, %3, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %2, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h), "=&v"(l)
+      : "s"(s), "v"(x0), "v"(x1), "v"(nz));
+  hi = h;
+  lo = l;
+}
+
+// one v_add_f32 (the SLP vectoriser would pack such sums through moves)
+MPV_DEV float add_f32(float a, float b) {
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Power-of-two scale mapping max|x| to (2^13, 2^14]; 1 for 0 / non-finite.
 MPV_DEV float pow2_scale(float maxabs) {
   if (!(maxabs > 0.0f) || !isfinite(maxabs)) return 1.0f;

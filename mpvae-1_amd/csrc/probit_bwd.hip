@@ -133,9 +133,10 @@ struct ElemCol {
   bool soft[4];
   float qm[4];  // d = E + qm: E - 1 for y = 0 (the sign of d logp/dE folded in), E otherwise
   float sga[4];   // e^{-5E} (y = 1) or e^{5E} as exp2(sga w) e^{-+5 C0}
-  float wp[4], wn[4];  // [y = 1], [y = 0]
+  float wp[4], wn[4];  // [y = 1], [y = 0] (1 or 0)
   bool pos[4];         // y = 1
-  float kp, kn;        // e^{-5 C0}, e^{5 C0} (the nonzero wp, wn)
+  float kp, kn;        // e^{-5 C0}, e^{5 C0}: the row's ranking coefficients
+                       // rkp = kp (-bP), rkn = kn bN carry them
 };
 
 // Four elements (columns) of one row at once, step-major so that the
@@ -146,17 +147,16 @@ struct ElemCol {
 // it with a wave-uniform test).  SOFT_RCP: a soft label's y/E - (1-y)/(1-E)
 // by hardware reciprocals (1 ulp) instead of IEEE divisions, whose
 // registers would spill the LDS-ring kernel.
+// rkp, rkn: the row's ranking coefficients of a positive / negative label,
+// kp (-betaP) and kn betaN (a binary block picks one per column instead of
+// forming wn rkn + wp rkp; elem_rank_coefs).
 template <bool SOFT = true, bool NANCHK = true, bool SOFT_RCP = false>
-MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 bP, f32x2 bN,
+MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 rkp, f32x2 rkn,
                        f32x2 (&out)[4]) {
   f32x2 zq[4], w[4], ez[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) zq[q] = pk_fma(splat2(t[q]), splat2(kZq), c.base[q]);
   probit_dw2xN_zq<4>(zq, w, ez);
-  const f32x2 nbP = -bP;
-  // the ranking coefficient of a positive / negative label of this row (a
-  // binary block picks one per column instead of forming wn bN + wp (-bP))
-  const f32x2 rkp = splat2(c.kp) * nbP, rkn = splat2(c.kn) * bN;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // E in the reference's rounding order (mpvae.py:171-180: cdf = 0.5 (1 +
@@ -185,20 +185,27 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
       dE = pk_fma(alpha, r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-    const f32x2 rk = SOFT ? pk_fma(splat2(c.wn[q]), bN, splat2(c.wp[q]) * nbP)
+    const f32x2 rk = SOFT ? pk_fma(splat2(c.wn[q]), rkn, splat2(c.wp[q]) * rkp)
                           : (c.pos[q] ? rkp : rkn);
     const f32x2 a = w[q] * c.sga[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
     out[q] = dE * ez[q];  // the coefficients carry kPhiK
   }
   // a degenerate row poisons every label, whatever its value (reference autograd)
-  if (NANCHK && (bP.x != bP.x || bP.y != bP.y)) {
+  // (rkp is NaN exactly when betaP is)
+  if (NANCHK && (rkp.x != rkp.x || rkp.y != rkp.y)) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (bP.x != bP.x) out[q].x = bP.x;
-      if (bP.y != bP.y) out[q].y = bP.y;
+      if (rkp.x != rkp.x) out[q].x = rkp.x;
+      if (rkp.y != rkp.y) out[q].y = rkp.y;
     }
   }
+}
+
+// The ranking coefficients of one row from its betaP, betaN (label, feature).
+MPV_DEV void elem_rank_coefs(const ElemCol& c, f32x2 bP, f32x2 bN, f32x2& rkp, f32x2& rkn) {
+  rkp = splat2(c.kp) * -bP;
+  rkn = splat2(c.kn) * bN;
 }
 
 // Inputs of one row s of the element pass: its six coefficients (label .x,
@@ -252,8 +259,8 @@ MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, boo
     const float sgx = (yv == 1.0f ? -5.0f : 5.0f) * 1.4426950408889634f;
     ec.sga[q] = sgx * kEh;
     // the constant factor e^{-+5 C0} of e^{-+5E} rides on the label weights
-    ec.wp[q] = yv == 1.0f ? ec.kp : 0.0f;
-    ec.wn[q] = yv == 0.0f ? ec.kn : 0.0f;
+    ec.wp[q] = yv == 1.0f ? 1.0f : 0.0f;
+    ec.wn[q] = yv == 0.0f ? 1.0f : 0.0f;
     ec.pos[q] = yv == 1.0f;
   }
 }
@@ -297,7 +304,9 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
       const int64_t cb = (int64_t)b * S + s;
       float G[4];
       f32x2 g2[4];
-      d_elem2x4(cur.t, ec, cur.alpha, cur.bP, cur.bN, g2);
+      f32x2 rkp, rkn;
+      elem_rank_coefs(ec, cur.bP, cur.bN, rkp, rkn);
+      d_elem2x4(cur.t, ec, cur.alpha, rkp, rkn, g2);
       // column sums: pad columns (finite, never published) need no mask
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -305,6 +314,8 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
         G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
       }
       if (PLANES) {
+        // (split2_f16 / add_f32 here, as in elem_ring_rows: C3 element pass
+        // +4 %, the per-column branches leave the asm blocks unscheduled)
         uint16_t h[4], l[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
@@ -363,12 +374,21 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
 // ops behind s_nop: its per-column soft-label branches split the row into
 // basic blocks the scheduler cannot interleave across, and without them hipcc
 // drains its lookahead loads every row: DESIGN.md section 3.)
-constexpr int kElemRing = 6;       // T rows in flight per wave (1 KB each)
+constexpr int kElemRing = 8;       // T rows in flight per wave (1 KB each; 8: 3 waves per SIMD)
 constexpr int kElemRingRows = 256;  // rows per sub-chunk (the coefficient copy)
 constexpr int kElemRingMinRows = 64;  // rows per block at least (plan_bwd)
 // The rows of one sub-chunk [sb, sb + nrows) for one wave; SOFT: the block
 // holds soft labels (block-uniform, so either loop is one basic block).
-template <bool SOFT>
+// MASK: some lane of the wave has columns past L or past the planes (their G is
+// zeroed, their stores skipped).  NANCHK: some row of the sub-chunk is
+// degenerate (its NaN poisons every label of that row).  The loop is bound by
+// VALU issue (~95 % busy at C4, profiles/r05_elem_valu_pmc.json), so the row
+// sums and the f16 split are one instruction each (asm: hipcc's SLP
+// vectoriser otherwise packs the sums through register moves and splits by
+// convert / convert back / subtract), the coefficients sit in LDS as the
+// (label, feature) pairs the packed math takes, and the checks that do not
+// apply to a wave or a sub-chunk are compiled out.
+template <bool SOFT, bool MASK, bool NANCHK>
 MPV_DEV void elem_ring_rows(const ElemParams& p, const ElemCol& ec, const bool (&ok)[4], bool live,
                             int b, int sb, int nrows, int c0, float gs, uint32_t voff,
                             float* myring, const float (*cf)[8], f32x2 (&sg2)[4]) {
@@ -382,47 +402,63 @@ MPV_DEV void elem_ring_rows(const ElemParams& p, const ElemCol& ec, const bool (
   };
   const int pro = min(NR, nrows);
   for (int r = 0; r < pro; ++r) issue(r);
-  for (int r = 0; r < nrows; ++r) {
-    // ops issued after row r's DMA: the DMAs of rows r+1 .. min(r+NR-1,
-    // last) and the two plane stores of each row max(0, r-NR+1) .. r-1;
-    // vector memory ops retire in issue order
-    wait_vmcnt_dyn(min(NR - 1, nrows - 1 - r) + 2 * min(r, NR - 1));
+  auto row = [&](int r) {
     const f32x4 tv = *reinterpret_cast<const f32x4*>(myring + (r % NR) * 256 + lane * 4);
     const f32x4 ca = *reinterpret_cast<const f32x4*>(&cf[r][0]);
-    const f32x2 cb = *reinterpret_cast<const f32x2*>(&cf[r][4]);
-    const f32x2 alpha = f32x2{ca[0], ca[3]}, bP = f32x2{ca[1], cb[0]}, bN = f32x2{ca[2], cb[1]};
+    const f32x2 rkn = *reinterpret_cast<const f32x2*>(&cf[r][4]);
+    const f32x2 alpha = f32x2{ca[0], ca[1]}, rkp = f32x2{ca[2], ca[3]};
     const float t[4] = {tv[0], tv[1], tv[2], tv[3]};
     f32x2 g2[4];
-    d_elem2x4<SOFT, false, true>(t, ec, alpha, bP, bN, g2);
-    // a degenerate row poisons every label (the row's bP is wave-uniform)
-    if (__builtin_amdgcn_readfirstlane((bP.x != bP.x || bP.y != bP.y) ? 1 : 0)) {
+    d_elem2x4<SOFT, false, true>(t, ec, alpha, rkp, rkn, g2);
+    // a degenerate row poisons every label (the row's rkp is wave-uniform)
+    if (NANCHK && __builtin_amdgcn_readfirstlane((rkp.x != rkp.x || rkp.y != rkp.y) ? 1 : 0)) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if (bP.x != bP.x) g2[q].x = bP.x;
-        if (bP.y != bP.y) g2[q].y = bP.y;
+        if (rkp.x != rkp.x) g2[q].x = rkp.x;
+        if (rkp.y != rkp.y) g2[q].y = rkp.y;
       }
     }
     float G[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       sg2[q] = sg2[q] + g2[q];
-      G[q] = ok[q] ? g2[q].x + g2[q].y : 0.0f;
+      G[q] = add_f32(g2[q].x, g2[q].y);
+      if (MASK && !ok[q]) G[q] = 0.0f;
     }
-    uint16_t h[4], l[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) split_f16(G[q], gs, h[q], l[q]);
+    uint32_t hv[2], lv[2];
+    split2_f16(G[0], G[1], gs, hv[0], lv[0]);
+    split2_f16(G[2], G[3], gs, hv[1], lv[1]);
     const int64_t o = chunked_index(rowb + r, p.gld, live ? c0 : 0);
-    const s16x4 hv{(short)h[0], (short)h[1], (short)h[2], (short)h[3]};
-    const s16x4 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3]};
-    if (live) {  // nontemporal plane stores (the element pass -2 %, round 2)
-      __builtin_nontemporal_store(hv, reinterpret_cast<s16x4*>(p.g + o));
-      __builtin_nontemporal_store(lv, reinterpret_cast<s16x4*>(p.g + o + kLoOff));
+    if (!MASK || live) {  // nontemporal plane stores (the element pass -2 %, round 2)
+      __builtin_nontemporal_store(u32x2{hv[0], hv[1]}, reinterpret_cast<u32x2*>(p.g + o));
+      __builtin_nontemporal_store(u32x2{lv[0], lv[1]}, reinterpret_cast<u32x2*>(p.g + o + kLoOff));
     }
     if (r + NR < nrows) issue(r + NR);  // into the slot row r was just read from
+  };
+  // Before row r is read, the ops issued after its DMA are the DMAs of rows
+  // r+1 .. min(r+NR-1, last) and the two plane stores of each row
+  // max(0, r-NR+1) .. r-1 (vector memory ops retire in issue order).  Rows
+  // NR-1 .. nrows-NR wait for a constant count; the ramps use the run-time
+  // count (an s_waitcnt takes an immediate: a compare ladder).  Only the
+  // common loop (binary labels, full waves, no degenerate row) is peeled.
+  int r = 0;
+  if (!SOFT && !MASK && !NANCHK) {
+    for (; r < min(NR - 1, nrows); ++r) {
+      wait_vmcnt_dyn(min(NR - 1, nrows - 1 - r) + 2 * r);
+      row(r);
+    }
+    for (; r <= nrows - NR; ++r) {
+      wait_vmcnt<3 * (NR - 1)>();
+      row(r);
+    }
+  }
+  for (; r < nrows; ++r) {
+    wait_vmcnt_dyn(min(NR - 1, nrows - 1 - r) + 2 * min(r, NR - 1));
+    row(r);
   }
 }
 
-__global__ __launch_bounds__(256, 4) void bwd_elem_ring_kernel(ElemParams p) {
+__global__ __launch_bounds__(256, 3) void bwd_elem_ring_kernel(ElemParams p) {
   constexpr int NR = kElemRing, CR = kElemRingRows;
   __shared__ __attribute__((aligned(16))) float ring[4][NR][256];  // [wave][slot][1 KB]
   __shared__ __attribute__((aligned(16))) float cf[CR][8];  // alpha, bP, bN (label, feature)
@@ -443,6 +479,8 @@ __global__ __launch_bounds__(256, 4) void bwd_elem_ring_kernel(ElemParams p) {
   // every store instruction has a live lane, so it issues (the vmcnt
   // arithmetic of elem_ring_rows counts on that)
   const bool wave_live = (int)(blockIdx.z * 1024 + wid * 256) < p.Lc;
+  // every lane's four columns are labels (< L) and in the planes (< Lc)
+  const bool wave_full = (int)(blockIdx.z * 1024 + wid * 256 + 256) <= min(L, p.Lc);
   const bool live = c0 < p.Lc;
   const int s_begin = sc * p.rows_per_chunk;
   const int s_end = min(S, s_begin + p.rows_per_chunk);
@@ -453,15 +491,31 @@ __global__ __launch_bounds__(256, 4) void bwd_elem_ring_kernel(ElemParams p) {
   for (int sb = s_begin; sb < s_end; sb += CR) {  // sub-chunks of <= CR rows
     const int nrows = min(CR, s_end - sb);
     __syncthreads();  // the previous sub-chunk's cf reads are done
-#pragma unroll
-    for (int k = 0; k < 6; ++k)  // coef is [k][b][s] -> cf[row][k]
-      for (int r = tid; r < nrows; r += 256) cf[r][k] = p.coef[k * BS + (int64_t)b * S + sb + r];
-    __syncthreads();
+    // coef is [k][b][s]: cf[row] = alpha, rkp, rkn as (label, feature) pairs
+    bool nan_row = false;
+    for (int r = tid; r < nrows; r += 256) {
+      const int64_t o = (int64_t)b * S + sb + r;
+      const f32x2 alpha{p.coef[o], p.coef[3 * BS + o]};
+      const f32x2 bP{p.coef[BS + o], p.coef[4 * BS + o]};
+      const f32x2 bN{p.coef[2 * BS + o], p.coef[5 * BS + o]};
+      f32x2 rkp, rkn;
+      elem_rank_coefs(ec, bP, bN, rkp, rkn);
+      nan_row |= bP.x != bP.x || bP.y != bP.y;
+      *reinterpret_cast<f32x4*>(&cf[r][0]) = f32x4{alpha.x, alpha.y, rkp.x, rkp.y};
+      *reinterpret_cast<f32x2*>(&cf[r][4]) = rkn;
+    }
+    const bool nan_any = __syncthreads_or(nan_row) != 0;
     if (!wave_live) continue;
-    if (soft_any)
-      elem_ring_rows<true>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, &ring[wid][0][0], cf, sg2);
-    else
-      elem_ring_rows<false>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, &ring[wid][0][0], cf, sg2);
+    float* myring = &ring[wid][0][0];
+    if (soft_any || !wave_full || nan_any) {
+      if (soft_any)
+        elem_ring_rows<true, true, true>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, myring, cf, sg2);
+      else
+        elem_ring_rows<false, true, true>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, myring, cf, sg2);
+    } else {
+      elem_ring_rows<false, false, false>(p, ec, ok, live, b, sb, nrows, c0, gs, voff, myring, cf,
+                                          sg2);
+    }
   }
   // column sums of the block's rows -> colpart (the ring is free now)
   __syncthreads();
