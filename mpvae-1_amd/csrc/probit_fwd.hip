@@ -748,6 +748,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   for (int m = 0; m < TL; ++m)
 #pragma unroll
     for (int n = 0; n < TS; ++n) acc[m][n] = acc[m][n] * scale;  // t (exact: power of 2)
+  // wave-uniform: the T stash needs no per-lane row / label conditions
+  const bool t_plain = s0 + sbo * 16 >= s_own && s0 + (sbo + TS) * 16 <= S && n0 + BN <= L;
   // one label group per iteration, not unrolled (code size / live ranges):
   // the group's accumulators are always acc[0]; the rest rotate down after it
   // (round 2: unrolled by 2, 15 VGPRs spill; fully, 95.  Round 3's compiler
@@ -771,7 +773,16 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       __builtin_amdgcn_s_setprio(1);
     else
       __builtin_amdgcn_s_setprio(0);
-    if (p.T != nullptr) {
+    if (p.T != nullptr && t_plain) {
+      // every row of the wave is the tile's own and < S, every label < L:
+      // plain 16-B stores, no per-lane conditions (their exec-mask branches
+      // were ~50 scalar instructions per label group)
+#pragma unroll
+      for (int n = 0; n < TS; ++n) {
+        const int s = s0 + (sbo + n) * 16 + lr;
+        *reinterpret_cast<f32x4*>(p.T + ((int64_t)b * S + s) * p.ldT + n0 + lb) = am[n];
+      }
+    } else if (p.T != nullptr) {
       // T stash of this label group, at the top of its iteration (all 16
       // stores up front kept the prio-0 waves 4-8 K cycles in store issue)
 #pragma unroll
