@@ -3,8 +3,11 @@
 torch.profiler over a few steps of bench.py's step function, device kernels,
 memsets and memcpys grouped by the top-level op that issued them.
 
-  python tools/step_ops.py [--n-sample 512] [--dist]   (--dist: the sharded
-  path on a world-of-one RCCL group, as MPVAE_FORCE_DIST=1 bench.py)
+  python tools/step_ops.py [--n-sample 512]
+
+(The sharded path on a world-of-one RCCL group is profiled with a rocprofv3
+kernel trace of MPVAE_FORCE_DIST=1 bench.py instead: under torch.profiler that
+run reported no device activity.)
 """
 import argparse
 import json
@@ -19,20 +22,14 @@ import bench  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n-sample", type=int, default=512)
-ap.add_argument("--dist", action="store_true")
 ap.add_argument("--steps", type=int, default=3)
 cli = ap.parse_args()
-if cli.dist:
-    import torch.distributed as dist
-    os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=os.environ.get("MASTER_PORT", "29547"))
-    dist.init_process_group("nccl", device_id=torch.device("cuda:0"))
 dev = torch.device("cuda:0")
 L = z = 1024
 y, leaves = bench.make_inputs(L, z, 512, 50, dev)
 args = argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=cli.n_sample,
                           n_test_sample=cli.n_sample, mode="train", nll_coeff=0.1, c_coeff=200.0,
-                          mpvae_noise="philox", mpvae_shard=cli.dist, mpvae_force_exchange=cli.dist)
+                          mpvae_noise="philox")
 for it in range(3):
     bench.step(y, leaves, args, it)
 torch.cuda.synchronize()
@@ -50,6 +47,4 @@ for e in prof.key_averages():
         rows.append({"op": e.key, "calls_per_step": e.count / cli.steps,
                      "device_us_per_step": dt / cli.steps})
 rows.sort(key=lambda r: -r["device_us_per_step"])
-print(json.dumps({"n_sample": cli.n_sample, "dist": cli.dist, "ops": rows[:60]}, indent=1), flush=True)
-if cli.dist:
-    dist.destroy_process_group()
+print(json.dumps({"n_sample": cli.n_sample, "ops": rows[:60]}, indent=1), flush=True)
