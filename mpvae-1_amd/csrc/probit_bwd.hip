@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
 // drains its lookahead loads every row: DESIGN.md section 3.)
 constexpr int kElemRing = 8;       // T rows in flight per wave (1 KB each; 8: 3 waves per SIMD)
 constexpr int kElemRingRows = 256;  // rows per sub-chunk (the coefficient copy)
-constexpr int kElemRingMinRows = 64;  // rows per block at least (plan_bwd)
+constexpr int kElemRingMinRows = 128;  // rows per block at least (plan_bwd; 64: +0.3 % at S 512)
 // The rows of one sub-chunk [sb, sb + nrows) for one wave; SOFT: the block
 // holds soft labels (block-uniform, so either loop is one basic block).
 // MASK: some lane of the wave has columns past L or past the planes (their G is
