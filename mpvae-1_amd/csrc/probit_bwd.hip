@@ -361,8 +361,9 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
   }
 }
 
-// The element pass for 3xf16 planes when a block row covers 1024 columns
-// (L >= 1024: C4, C5).  T rows stream through a per-wave LDS ring by LDS-DMA
+// The element pass for 3xf16 planes when one thread row of a block covers a
+// whole label row (plan_bwd: TPR = cdiv(Lc, 4), so Lc > 512: C4, C5 and any
+// 512 < L < 1024, whose surplus waves are masked).  T rows stream through a per-wave LDS ring by LDS-DMA
 // (global_load_lds_dwordx4: a wave moves the 1 KB of a row its own 256
 // columns need, so no wave reads another's slot and the ring needs no
 // barrier); the row's six coefficients come from an LDS copy of the block's

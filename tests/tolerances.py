@@ -133,6 +133,17 @@ def record(test_id, errs):
                     + "\n")
 
 
+def record_json(test_id, obj):
+    """Append a structured record (any JSON-able object) of one case to
+    $MPVAE_RECORD_ERRS when that is set."""
+    import json
+    import os
+    path = os.environ.get("MPVAE_RECORD_ERRS")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test_id, "record": obj}) + "\n")
+
+
 def rel_err(a, b):
     import numpy as np
     a = np.asarray(a, np.float64)
