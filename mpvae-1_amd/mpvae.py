@@ -193,6 +193,33 @@ class VAE(nn.Module):
         return label_out, mu_e, lv_e, feat_out, mu_x, lv_x
 
 
+# Reference-exact CPU noise under sample sharding: every rank draws all
+# n_sample * B * z normals on its host (torch's CPU generator cannot skip ahead)
+# and keeps its 1/world slice.  Above WARN elements per step that is flagged;
+# above MAX (16 GiB of fp32 per rank per step, e.g. C5's 1.7e10 = 68.7 GB) it
+# is refused: args.mpvae_noise = "philox" draws each rank's own slice on the
+# device from a key shared across ranks (the single-device stream at any world).
+SHARDED_CPU_NOISE_WARN = 1 << 26
+SHARDED_CPU_NOISE_MAX = 1 << 32
+
+
+def _guard_sharded_cpu_noise(n, world):
+    if n > SHARDED_CPU_NOISE_MAX:
+        raise ValueError(
+            f"args.mpvae_noise='torch_cpu' with args.mpvae_shard draws the whole "
+            f"{n:.3g}-element noise tensor ({4 * n / 2 ** 30:.1f} GiB) on every one of the "
+            f"{world} ranks' hosts each step and uses 1/{world} of it; above "
+            f"{SHARDED_CPU_NOISE_MAX:.3g} elements that is refused -- use "
+            "args.mpvae_noise='philox' (per-rank device noise, the same stream at any world "
+            "size) or pass the noise tensor explicitly")
+    if n > SHARDED_CPU_NOISE_WARN:
+        import warnings
+        warnings.warn(f"args.mpvae_noise='torch_cpu' with args.mpvae_shard: each of the {world} "
+                      f"ranks draws all {n:.3g} normals on its host per step to keep the "
+                      "reference's CPU stream, and uses 1/world of them; "
+                      "args.mpvae_noise='philox' scales", stacklevel=4)
+
+
 def _noise_source(args, n_sample, B, z, shard, device):
     """(noise tensor or None, ElboConfig kwargs) for compute_loss."""
     mode = getattr(args, "mpvae_noise", "torch_cpu")
@@ -202,7 +229,11 @@ def _noise_source(args, n_sample, B, z, shard, device):
             raise ValueError(f"args.mpvae_noise must be {(n_sample, B, z)}, got {tuple(mode.shape)}")
         return mode[s0:s1].to(device=device, dtype=torch.float32), dict(noise="explicit")
     if mode == "torch_cpu":
-        # mpvae.py:162 -- same generator, same draw, same shape; then H2D
+        # mpvae.py:162 -- same generator, same draw, same shape; then H2D.
+        # Sharded, every rank must draw the WHOLE tensor to keep the
+        # single-device stream and then uses 1/world of it
+        if shard.exchange is not None:
+            _guard_sharded_cpu_noise(n_sample * B * z, shard.exchange.world)
         noise = torch.normal(0, 1, size=(n_sample, B, z))
         return noise[s0:s1].to(device), dict(noise="explicit")
     if mode == "philox":

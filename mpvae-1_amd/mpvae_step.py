@@ -172,17 +172,38 @@ class DeviceStepLR:
         self._host_lr = [float(g["lr"]) for g in opt.param_groups]  # as last synced / adopted
         self._hook = opt.register_state_dict_pre_hook(lambda _opt: self.sync())
         self._sched_state_dict, self._sched_step = sched.state_dict, sched.step
+        self._sched_load = sched.load_state_dict
 
         def state_dict():
             self.sync()
             return self._sched_state_dict()
+
+        def load_state_dict(state):
+            # a resumed scheduler checkpoint: the device epoch and
+            # lr follow it, so the decay boundaries are the checkpoint's and
+            # the next sync() does not write a stale epoch back
+            self._sched_load(state)
+            self._adopt(int(sched.last_epoch), [float(g["lr"]) for g in opt.param_groups])
 
         def step(*a, **k):
             raise RuntimeError("this StepLR is stepped on the device by TrainStep after every "
                                "applied update (fairsoft_train.py:142-145); do not call "
                                "scheduler.step() as well -- TrainStep.release_scheduler() hands "
                                "it back")
-        sched.state_dict, sched.step = state_dict, step
+        sched.state_dict, sched.step, sched.load_state_dict = state_dict, step, load_state_dict
+
+    def _adopt(self, epoch, lrs):
+        """Host values -> the device state, stream-ordered, without a host wait:
+        the lrs go through a pinned staging tensor (the caching host allocator
+        keeps it alive until the copy has run)."""
+        src = torch.tensor(lrs, dtype=torch.float64)
+        if self.lr.is_cuda:
+            src = src.pin_memory()
+        self.lr.copy_(src, non_blocking=True)
+        if epoch is not None:
+            self.last_epoch.fill_(epoch)
+            self._epoch0 = epoch
+        self._host_lr = list(lrs)
 
     def sync(self):
         """Copy the device lr / last_epoch into the optimizer and the scheduler."""
@@ -199,20 +220,21 @@ class DeviceStepLR:
 
     def adopt_host_lr(self):
         """A param group's lr changed on the host since the last sync: the
-        device lr takes it (host compare, non-blocking copy; no device sync)."""
+        device lr takes it (a host-side compare; the copy is stream-ordered from
+        a pinned staging tensor, so the host does not wait for the device)."""
         now = [float(g["lr"]) for g in self.opt.param_groups]
         if now != self._host_lr:
             import warnings
             warnings.warn("optimizer param_groups lr edited on the host while TrainStep owns "
                           "the StepLR: the device lr adopts the new value", stacklevel=3)
-            self.lr.copy_(torch.tensor(now, dtype=torch.float64), non_blocking=False)
-            self._host_lr = now
+            self._adopt(None, now)
 
     def release(self):
         """Sync, then hand the scheduler and optimizer back to host control."""
         lrs = self.sync()
         self._hook.remove()
         self.sched.state_dict, self.sched.step = self._sched_state_dict, self._sched_step
+        self.sched.load_state_dict = self._sched_load
         return lrs
 
 
@@ -328,10 +350,16 @@ class TrainStep:
 
     def release_scheduler(self):
         """Sync and give the StepLR back to host control (its step() works
-        again); TrainStep then no longer steps it."""
+        again); TrainStep then no longer steps it.  A graph captured before
+        holds the device lr / epoch and the scheduler step in its Adam launches
+        (ADVICE r05): it is dropped, so later calls run eagerly on the host lr
+        until capture() records the step again."""
         if self.sched is None:
             return None
         lrs, self.sched = self.sched.release(), None
+        if self.graph is not None:
+            self.graph = None
+            self.label = self.feat = self.out = None
         return lrs
 
     def __call__(self, label, feat):

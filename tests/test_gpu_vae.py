@@ -339,6 +339,38 @@ def test_train_step_graph_replays_match_eager():
     assert tg.sync_scheduler() == te.sync_scheduler() == [1e-3 * 0.5 * 0.5]
 
 
+def test_release_scheduler_drops_the_captured_graph():
+    """a graph captured while TrainStep owned the StepLR steps the
+    device lr inside its Adam launch.  release_scheduler() drops it, so the
+    next call runs eagerly on the host's param_groups lr: with lr set to 0
+    on the host the parameters stay as they are (a replay would have moved
+    them by the device lr)."""
+    import mpvae_step
+    B, F_, L = 16, 30, 8
+    a = _args(feature_dim=F_, label_dim=L, z_dim=L, latent_dim=8, keep_prob=0.0,
+              n_train_sample=32, mpvae_noise="philox",
+              mpvae_seed=torch.tensor([5], dtype=torch.int64, device=DEV))
+    m = _seeded_model(a, seed=4).to(DEV).train()
+    o = torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=True)
+    sch = torch.optim.lr_scheduler.StepLR(o, 2, 0.5)
+    ts = mpvae_step.TrainStep(m, o, a, scheduler=sch)
+    g = torch.Generator().manual_seed(3)
+    y = (torch.rand(B, L, generator=g) < 0.3).float()
+    y[:, 0], y[:, 1] = 1, 0
+    batch = (y.to(DEV), torch.randn(B, F_, generator=g).to(DEV))
+    ts.capture(*batch, warmup=1)
+    ts(*batch)  # a replay: the device lr is in use
+    assert ts.release_scheduler() == [o.param_groups[0]["lr"]]
+    assert ts.graph is None
+    o.param_groups[0]["lr"] = 0.0
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    ts(*batch)
+    torch.cuda.synchronize()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    sch.step()  # the host scheduler is usable again
+
+
 def test_native_adam_matches_torch_fused_adam():
     """mpvae_step.adam_step (csrc/adam.hip, one launch) against torch's fused
     capturable Adam on the same parameters and gradients: fp32 tensors of the

@@ -197,3 +197,60 @@ def test_device_steplr_keeps_host_objects_consistent():
     assert d.release() == [1e-2]
     sched.step()  # host control again
     assert sched.last_epoch == 3
+
+
+def test_device_steplr_follows_a_loaded_scheduler_checkpoint():
+    """sched.load_state_dict while TrainStep owns the StepLR moves
+    the device epoch and lr to the checkpoint's (decay boundaries from the
+    checkpoint), and the next sync() does not write a stale epoch back."""
+    import mpvae_step
+    p = torch.nn.Parameter(torch.zeros(3))
+    opt = torch.optim.Adam([p], lr=1e-3, fused=True)
+    sched = torch.optim.lr_scheduler.StepLR(opt, 2, 0.5)
+    # a checkpoint taken after 5 host scheduler steps
+    p2 = torch.nn.Parameter(torch.zeros(3))
+    opt2 = torch.optim.Adam([p2], lr=1e-3, fused=True)
+    sched2 = torch.optim.lr_scheduler.StepLR(opt2, 2, 0.5)
+    for _ in range(5):
+        opt2.step()
+        sched2.step()
+    ckpt_opt, ckpt_sched = opt2.state_dict(), sched2.state_dict()
+    d = mpvae_step.DeviceStepLR(sched, opt)
+    opt.load_state_dict(ckpt_opt)
+    sched.load_state_dict(ckpt_sched)
+    assert int(d.last_epoch) == 5 and d.lr.tolist() == [opt2.param_groups[0]["lr"]] == [2.5e-4]
+    assert d.sync() == [2.5e-4] and sched.last_epoch == 5
+    assert sched.state_dict()["last_epoch"] == 5
+    d.release()
+    assert sched.load_state_dict.__func__ is torch.optim.lr_scheduler.StepLR.load_state_dict
+
+
+def test_sharded_reference_noise_guard(monkeypatch):
+    """args.mpvae_noise='torch_cpu' under sample sharding
+    draws the whole (n_sample, B, z) tensor on every rank's host; above
+    SHARDED_CPU_NOISE_MAX elements compute_loss's noise source refuses (before
+    drawing anything), above SHARDED_CPU_NOISE_WARN it warns; unsharded it is
+    the reference's draw as before."""
+    import warnings
+    from types import SimpleNamespace
+    ex = SimpleNamespace(world=8)
+    args = argparse.Namespace(mpvae_noise="torch_cpu")
+    big = SimpleNamespace(S_local=1024, s_offset=0, exchange=ex)
+    # C5: n_sample 8192, B 512, z 4096 -> 1.7e10 normals per rank per step
+    with pytest.raises(ValueError, match="philox"):
+        mpvae._noise_source(args, 8192, 512, 4096, big, "cpu")
+    monkeypatch.setattr(mpvae, "SHARDED_CPU_NOISE_WARN", 1000)
+    small = SimpleNamespace(S_local=4, s_offset=4, exchange=ex)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        noise, kw = mpvae._noise_source(args, 32, 8, 5, small, "cpu")
+    assert any("philox" in str(x.message) for x in w)
+    assert tuple(noise.shape) == (4, 8, 5) and kw == dict(noise="explicit")
+    unsharded = SimpleNamespace(S_local=32, s_offset=0, exchange=None)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        torch.manual_seed(3)
+        noise, _ = mpvae._noise_source(args, 32, 8, 5, unsharded, "cpu")
+    assert not w
+    torch.manual_seed(3)
+    assert torch.equal(noise, torch.normal(0, 1, size=(32, 8, 5)))
