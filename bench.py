@@ -69,6 +69,23 @@ DEFAULT_STEPS = {"c2": (200, 5), "c3": (200, 5), "c4": (200, 5), "c5": (10, 2)}
 # the probit kernels of the small configurations (L, z <= 128) are VALU-bound
 # (SURVEY.md section 8(d)): their roofline is the VALU ceiling
 SMALL_LZ = 128
+# The algorithmic VALU floor of the two element-wise kernels, in lane-
+# instructions per label-sample (both branches; a packed fp32 op serving two
+# elements counts 1/2 per element), counted from the formulation the kernels
+# evaluate (csrc/mpv_common.h probit_w2xN_zq / probit_dw2xN_zq and their
+# callers), so that frac_algorithmic prices algorithmic work, not whatever a
+# kernel executes:
+#   forward, per element and branch: argument 0.5, t = rcp(fma) 2, degree-6 P
+#   3, exponent 0.5, exp 1, erfc 0.5, 1 - erfc 0.5, copysign 1, w 0.5, E in
+#   the reference's order 1, BCE operand 0.5, ranking exponent 0.5, exp 1, the
+#   log of a 4-label product 0.625, row sum 0.125, P / N sums 1, column sum
+#   0.5 = 14.75; x 2 branches = 29.5 (C4 executes 43.6);
+#   element pass, per element and branch: argument 0.5, t 2, degree-6 Q 3,
+#   -z^2 0.5, exp 1, erfc 1.5, copysign 1, w 0.5, E 1, d 0.5, rcp 1, dE 0.5,
+#   ranking select 1, exponent 0.5, exp 1, fma 0.5, x exp(-z^2) 0.5 = 16.5,
+#   plus the column sum, G = dE + dE_x and its 3xf16 split 3.5 = 20; x 2 = 40
+#   (C4 executes 42.5).
+VALU_FLOOR_PER_LS = {"probit_fwd": 29.5, "bwd_elem": 40.0}
 
 
 def log(*a):
@@ -133,10 +150,12 @@ def step(y, leaves, args, it):
 
 def graph_steps(y, leaves, args, warmup, steps):
     """Capture one fwd+bwd step in a HIP graph and time `steps` replays.  The
-    Philox key is a device tensor advanced inside the graph, so every replay
+    Philox key is a device tensor that the step's own finalize launch advances
+    after the noise has read it (args.mpvae_seed_advance), so every replay
     draws fresh noise (tests/test_gpu_parity.py checks replays against eager)."""
     seed = torch.tensor([0x5EED0000], dtype=torch.int64, device=y.device)
     args.mpvae_seed = seed
+    args.mpvae_seed_advance = True
     # fresh leaves: their AccumulateGrad nodes are created on the capture's
     # side stream, not on the default stream of the eager pass
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in leaves.items()}
@@ -144,7 +163,6 @@ def graph_steps(y, leaves, args, warmup, steps):
     def one():
         for v in leaves.values():
             v.grad = None
-        seed.add_(1)
         if args.mode != "train":
             with torch.no_grad():
                 return mpvae.compute_loss(y, *[leaves[k] for k in ORDER], args)
@@ -195,12 +213,23 @@ def roofline(times, S_local, B, L, z, steps, gemm, valu=None):
         per = (valu or {}).get(dom)
         pk = VALU_PEAK / 1e12
         achieved = per / avg_s / 1e12 if per else None
+        ls = S_local * B * L
         res = {"kernel": dom, "bound": "valu", "achieved": achieved, "peak": pk,
                "unit": "Tlane-instr/s", "frac": achieved / pk if achieved else None,
                "traffic": None, "avg_ms": round(avg_s * 1e3, 4),
                "peak_basis": "VALU: 157.3 TFLOPS fp32 vector / 2 = one lane-instruction per "
                              "lane per cycle at 2.4 GHz (packed ops count once, as in "
-                             "SQ_INSTS_VALU)"}
+                             "SQ_INSTS_VALU)",
+               "valu_executed_per_ls": per / ls if per else None}
+        # the same kernel priced on its ALGORITHMIC instruction floor
+        # (VALU_FLOOR_PER_LS): executed-count fractions reward extra work
+        if dom in VALU_FLOOR_PER_LS:
+            res["frac_algorithmic"] = VALU_FLOOR_PER_LS[dom] * ls / avg_s / VALU_PEAK
+            res["valu_floor_per_ls"] = VALU_FLOOR_PER_LS[dom]
+        alg = sum(VALU_FLOOR_PER_LS[k] * ls * times[k][0] for k in VALU_FLOOR_PER_LS
+                  if k in times) / steps
+        res["step_frac_algorithmic"] = alg / (sum(v[1] for v in times.values()) / steps / 1e3) \
+            / VALU_PEAK
         if valu:  # the whole step: every profiled kernel's lane-instructions
             tot = sum(valu.get(k, 0.0) * times[k][0] for k in times) / steps
             step_s = sum(v[1] for v in times.values()) / steps / 1e3

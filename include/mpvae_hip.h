@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define MPV_ABI_VERSION 9  /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
+#define MPV_ABI_VERSION 10 /* 4: device-memory Philox keys (mpv_noise_philox*_dev);
                               5: T rows padded to roundup(L, 4) floats;
                               6: mpv_linear (the VAE's Linear layers); mpv_bwd_args
                                  dR64 and kl;
@@ -43,7 +43,12 @@ extern "C" {
                               9: mpv_adam_step reads the step count without
                                  advancing it (mpv_adam_finish does, with the
                                  update counter and a device StepLR); lr may
-                                 live in device memory */
+                                 live in device memory;
+                             10: mpv_probit_finalize_shards (the cross-shard
+                                 combine folded into the finalize launch); only
+                                 the live slots of gscal are read (mpv_kl_bwd_args
+                                 .live); mpv_noise_philox_f16_split;
+                                 mpv_final_args.seed_advance */
 
 enum mpv_status { MPV_OK = 0, MPV_EINVAL = 1, MPV_ELAUNCH = 2 };
 enum mpv_dtype { MPV_F32 = 0, MPV_F64 = 1 };
@@ -129,6 +134,16 @@ int mpv_noise_philox_f16(const mpv_shape* shape, uint64_t seed, uint64_t offset,
 int mpv_noise_philox_f16_dev(const mpv_shape* shape, const uint64_t* seed_dev, uint64_t offset,
                              const mpv_split16* out, void* stream);
 
+/* mpv_noise_philox_f16 (seed_dev NULL: the key `seed`) or mpv_noise_philox_f16_dev
+ * (the key read from seed_dev), and mpv_split_f16 of a small operand x (rows *
+ * cols <= 16384: r_sqrt_sigma at L, z <= 128) into x_out, in ONE launch: the
+ * split runs in extra workgroups beside the noise's.  The same outputs as the
+ * two calls. */
+int mpv_noise_philox_f16_split(const mpv_shape* shape, uint64_t seed, const uint64_t* seed_dev,
+                               uint64_t offset, const mpv_split16* out, const void* x,
+                               int x_dtype, int64_t rows, int64_t cols,
+                               const mpv_split16* x_out, void* stream);
+
 /* Element-wise dtype conversion; replaces r_sqrt_sigma.T.float() (mpvae.py:165)
  * and the fp32 -> fp64 cast of its gradient in autograd. */
 int mpv_convert(const void* src, int src_dtype, void* dst, int dst_dtype, int64_t n,
@@ -185,11 +200,21 @@ typedef struct mpv_final_args {
   float* kl;
   float* indiv_prob;        /* (B,L) = mean_s E_x  (mpvae.py:203) */
   float* indiv_prob_label;  /* (B,L) = mean_s E    (mpvae.py:204) */
+  uint64_t* seed_advance;   /* a device Philox key this step's noise has read, advanced by 1
+                               in the finalize launch (the next step draws fresh noise
+                               with no launch of its own), or NULL */
 } mpv_final_args;
 
 /* Replaces mpvae.py:147-148 (KL), :188-190 (log-sum-exp nll), :122 (ranking
  * mean), :203-210 (indiv_prob*, total).  `shape` gives B, L, S_total. */
 int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* args, void* stream);
+
+/* mpv_bstat_combine + mpv_probit_finalize in one launch (the sample-sharded
+ * path): `slots` holds the shards' bstat as (nslots, 6, B) (the all-reduced
+ * slot buffer), combined exactly into `bstat_out` (6, B) for the backward;
+ * `args->bstat` is ignored, `args->colsum` is the all-reduced (2, B, L). */
+int mpv_probit_finalize_shards(const mpv_shape* shape, const float* slots, int64_t nslots,
+                               float* bstat_out, const mpv_final_args* args, void* stream);
 
 /* --------------------------------------------------------------- backward */
 struct mpv_kl_bwd_args;  /* below */
@@ -206,7 +231,9 @@ typedef struct mpv_bwd_args {
                                   the workspace instead) */
   const float* rowstat;        /* (6,B,S_local) from the forward */
   const float* bstat;          /* (6,B) GLOBAL statistics */
-  const float* gscal;          /* (6) device: upstream grads, mpv_gslot order */
+  const float* gscal;          /* device: upstream grads, mpv_gslot order; a slot whose
+                                  MPV_LIVE bit is clear is not read (its gradient is 0),
+                                  so (6) floats, or just (1) when only MPV_G_TOTAL is live */
   const float* g_indiv;        /* (B,L) grad of indiv_prob, or NULL */
   const float* g_indiv_label;  /* (B,L) grad of indiv_prob_label, or NULL */
   float nll_coeff, c_coeff;
@@ -232,11 +259,12 @@ typedef struct mpv_kl_bwd_args {
   const float* fx_mu;
   const float* fx_logvar;
   int64_t B, d;
-  const float* gscal;  /* (6) device, mpv_gslot order; uses TOTAL and KL */
+  const float* gscal;  /* device, mpv_gslot order; uses TOTAL and KL where live */
   float* g_fe_mu;
   float* g_fe_logvar;
   float* g_fx_mu;
   float* g_fx_logvar;
+  int live;            /* MPV_LIVE bits of gscal (slots not live are not read) */
 } mpv_kl_bwd_args;
 
 /* Replaces autograd through the KL term, mpvae.py:147-148. */

@@ -369,6 +369,28 @@ MPV_DEV float block_reduce(float v, float* red) {
   return r;
 }
 
+// N block reductions of the same kind with one barrier pair (`red` >= 16 N
+// floats); each value is combined in the same order as by block_reduce.
+template <int N, bool IS_MAX>
+MPV_DEV void block_reduce_n(float (&v)[N], float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = IS_MAX ? wave_max(v[k]) : wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[k * 16 + wid] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float r = IS_MAX ? -INFINITY : 0.0f;
+    for (int i = 0; i < nw; ++i) r = IS_MAX ? fmaxf(r, red[k * 16 + i]) : r + red[k * 16 + i];
+    v[k] = r;
+  }
+}
+
 // Two block reductions of the same kind at the cost of one (`red` >= 32
 // floats); each value is combined in the same order as by block_reduce.
 template <bool IS_MAX>
@@ -394,7 +416,10 @@ MPV_DEV void block_reduce2(float& a, float& b, float* red) {
 template <typename KlArgs>
 MPV_DEV void kl_bwd_range(const KlArgs& a, int64_t i0, int64_t stride) {
   const int64_t n = a.B * a.d;
-  const float g = a.gscal[MPV_G_KL] + kKlWeight * a.gscal[MPV_G_TOTAL];
+  // a slot not live is not read (mpv_kl_bwd_args.live): its gradient is 0
+  const float gk = (a.live & MPV_LIVE(MPV_G_KL)) ? a.gscal[MPV_G_KL] : 0.0f;
+  const float gt = (a.live & MPV_LIVE(MPV_G_TOTAL)) ? a.gscal[MPV_G_TOTAL] : 0.0f;
+  const float g = gk + kKlWeight * gt;
   const float s = 0.5f * g / (float)a.B;
   for (int64_t i = i0; i < n; i += stride) {
     const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
@@ -462,6 +487,37 @@ MPV_DEV float pow2_scale(float maxabs) {
   int e;
   frexpf(maxabs, &e);           // maxabs = m * 2^e, m in [0.5, 1)
   return ldexpf(1.0f, 14 - e);  // maxabs * s in [2^13, 2^14)
+}
+
+// Exact combine of row b of per-shard statistics gathered as (R, 6, B):
+// M = max m_r, Z = sum Z_r exp(m_r - M), the ranking sums add
+// (mpv_bstat_combine, and the sharded finalize in the same order).
+MPV_DEV void bstat_combine_row(const float* __restrict__ g, int64_t R, int64_t B, int64_t b,
+                               float (&v)[6]) {
+#pragma unroll
+  for (int br = 0; br < 2; ++br) {
+    const int mi = 2 * br, zi = 2 * br + 1;
+    float M = -INFINITY;
+    for (int64_t r = 0; r < R; ++r) M = fmaxf(M, g[(r * 6 + mi) * B + b]);
+    float Z = 0.0f;
+    for (int64_t r = 0; r < R; ++r) Z += g[(r * 6 + zi) * B + b] * expf(g[(r * 6 + mi) * B + b] - M);
+    v[mi] = M;
+    v[zi] = Z;
+  }
+  for (int k = 4; k < 6; ++k) {
+    float acc = 0.0f;
+    for (int64_t r = 0; r < R; ++r) acc += g[(r * 6 + k) * B + b];
+    v[k] = acc;
+  }
+}
+
+// pow2_scale of max(bound[0..n)), computed by one wave (every lane active): the
+// same bits in every wave of every kernel that needs it (a max is exact in any
+// order), so the G planes' scale needs no launch of its own (round 6).
+MPV_DEV float wave_pow2_scale(const float* __restrict__ bound, int n) {
+  float m = 0.0f;
+  for (int i = threadIdx.x & 63; i < n; i += 64) m = fmaxf(m, bound[i]);
+  return pow2_scale(wave_max(m));
 }
 
 MPV_DEV f16x8 as_f16x8(s16x8 v) { return __builtin_bit_cast(f16x8, v); }

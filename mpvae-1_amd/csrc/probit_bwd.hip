@@ -28,7 +28,6 @@ int launch_sum_slabs(const float* in, int64_t nslab, int64_t n, void* out, int o
 int launch_sum_slabs_pair(const float* in0, int64_t nslab0, int64_t n0, void* out0,
                           int out0_dtype, const float* in1, int64_t nslab1, int64_t n1,
                           void* out1, int out1_dtype, hipStream_t s);
-int launch_scale(const float* block_max, int n, float* scale, hipStream_t s);
 
 // Upper bounds used for the G scale (3xf16): for E = Phi(u)(1-1e-6)+0.5e-6,
 // sup_u phi(u) |y/E - (1-y)/(1-E)| < 4.5 (inverse Mills ratio capped by the
@@ -47,7 +46,7 @@ __global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
     const float* __restrict__ gscal, const float* __restrict__ gI, const float* __restrict__ gIL,
     float* __restrict__ coef, float* __restrict__ gbound, int S, int B, int L, float S_total,
     float nll_coeff, float c_coeff, int live, mpv_kl_bwd_args kl, int kl_blocks) {
-  __shared__ float red[32];
+  __shared__ float red[48];
   if ((int)blockIdx.x >= B) {  // the extra workgroups: the KL backward (mpv_bwd_args.kl)
     kl_bwd_range(kl, (int64_t)(blockIdx.x - B) * blockDim.x + threadIdx.x,
                  (int64_t)kl_blocks * blockDim.x);
@@ -62,12 +61,28 @@ __global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
     nn += (v == 0.0f) ? 1.0f : 0.0f;
     gi = fmaxf(gi, (gI ? fabsf(gI[o]) : 0.0f) + (gIL ? fabsf(gIL[o]) : 0.0f));
   }
-  block_reduce2<false>(np, nn, red);
-  gi = block_reduce<true>(gi, red);
+  {  // the two counts and the max with one barrier pair (block_reduce's orders)
+    const int lane = tid & 63, wid = tid >> 6, nw = (blockDim.x + 63) >> 6;
+    np = wave_sum(np);
+    nn = wave_sum(nn);
+    gi = wave_max(gi);
+    __syncthreads();
+    if (lane == 0) red[wid] = np, red[16 + wid] = nn, red[32 + wid] = gi;
+    __syncthreads();
+    np = nn = 0.0f;
+    gi = -INFINITY;
+    for (int i = 0; i < nw; ++i) {
+      np += red[i];
+      nn += red[16 + i];
+      gi = fmaxf(gi, red[32 + i]);
+    }
+  }
   const float nrm = np * nn;
-  const float gt = gscal[MPV_G_TOTAL];
-  const float gn[2] = {gscal[MPV_G_NLL] + nll_coeff * gt, gscal[MPV_G_NLL_X] + nll_coeff * gt};
-  const float gc[2] = {gscal[MPV_G_C] + c_coeff * gt, gscal[MPV_G_C_X] + c_coeff * gt};
+  // only live slots are read (gscal may hold just the TOTAL slot)
+  auto gs = [&](int k) { return (live & MPV_LIVE(k)) ? gscal[k] : 0.0f; };
+  const float gt = gs(MPV_G_TOTAL);
+  const float gn[2] = {gs(MPV_G_NLL) + nll_coeff * gt, gs(MPV_G_NLL_X) + nll_coeff * gt};
+  const float gc[2] = {gs(MPV_G_C) + c_coeff * gt, gs(MPV_G_C_X) + c_coeff * gt};
   const bool clive[2] = {(live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C))) != 0,
                          (live & (MPV_LIVE(MPV_G_TOTAL) | MPV_LIVE(MPV_G_C_X))) != 0};
   const float inv_B = 1.0f / (float)B;
@@ -112,10 +127,10 @@ struct ElemParams {
   const float* coef;
   float* T;          // (B*S, ldT)
   uint16_t* g;       // chunked 3xf16 output planes (B*S rows of gld halves), or NULL: fp32 G over T
-  const float* g_scale;
+  const float* g_bound;  // (B) per-row bounds of |G|: the planes' scale (wave_pow2_scale)
   int64_t gld;
   float* colpart;  // [nSc][2][B][L]
-  int S, B, L, Lc;  // Lc: columns covered (L, or gld/2 for planes: pads get zeros)
+  int S, B, L, Lc;  // Lc: columns covered (L rounded up to 4 for planes: pads get G = 0)
   int ldT;          // t_cols(L)
   int TPR, RPI, rows_per_chunk;
   float inv_S;
@@ -271,7 +286,10 @@ MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, boo
 // Otherwise (L < 1024: C2, C3) they are per-lane, 12 more VGPRs than fit in
 // 128: those instantiations run at 3 waves per SIMD instead of spilling.
 constexpr int kElemLookahead = 1;
-constexpr int kElemMinRows = 16;  // minimum T rows per thread (C2 -6 %)
+#ifndef MPV_ELEM_MIN_ROWS
+#define MPV_ELEM_MIN_ROWS 16
+#endif
+constexpr int kElemMinRows = MPV_ELEM_MIN_ROWS;  // minimum T rows per thread (C2 -6 %)
 template <bool VEC, bool PLANES, bool ONE>
 __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p) {
   constexpr int LA = kElemLookahead;
@@ -282,7 +300,7 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
   const bool active = rsub < p.RPI;
   const int c0 = blockIdx.z * 1024 + cq * 4;
   const int S = p.S, B = p.B, L = p.L;
-  const float gs = PLANES ? *p.g_scale : 1.0f;
+  const float gs = PLANES ? wave_pow2_scale(p.g_bound, p.B) : 1.0f;
 
   bool ok[4];
   ElemCol ec;
@@ -467,7 +485,7 @@ __global__ __launch_bounds__(256, 3) void bwd_elem_ring_kernel(ElemParams p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.z * 1024 + tid * 4;
   const int S = p.S, B = p.B, L = p.L;
-  const float gs = *p.g_scale;
+  const float gs = wave_pow2_scale(p.g_bound, B);
   bool ok[4];
   ElemCol ec;
   elem_col_setup(p, b, c0, true, ok, ec);
@@ -553,7 +571,7 @@ __global__ __launch_bounds__(256, 3) void bwd_elem_ring_kernel(ElemParams p) {
 // same for A and B.
 struct Dr16Params {
   const uint16_t* g;    // chunked G planes, rows b*S + s, gld halves per row
-  const float* g_scale;
+  const float* g_bound;  // (B) per-row bounds of |G|: the planes' scale (wave_pow2_scale)
   int64_t gld;
   mpv_split16 eps16;    // rows b*S + s
   float* slab;          // [nKc][L][z]
@@ -702,7 +720,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16_kernel(Dr16Params p) {
                                                            acc[m][n], 0, 0, 0);
       }
   }
-  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
+  const float inv = 1.0f / (wave_pow2_scale(p.g_bound, p.B) * *p.eps16.scale);
   // D[i = l][j = z]: row = lg*4 + reg, col = lr
 #pragma unroll
   for (int m = 0; m < TM; ++m)
@@ -992,7 +1010,7 @@ __global__ __launch_bounds__(WM* WN * 64, 1) void dR16s_kernel(Dr16Params p) {
       DR_STAMP(i, 5);
     }
   }
-  const float inv = 1.0f / (*p.g_scale * *p.eps16.scale);
+  const float inv = 1.0f / (wave_pow2_scale(p.g_bound, p.B) * *p.eps16.scale);
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
@@ -1159,7 +1177,7 @@ __global__ __launch_bounds__(256) void dR_gemm_kernel(DrParams p) {
 // ------------------------------------------------------------------- plans
 struct BwdPlan {
   int dr_tile;                                  // dR output tile edge
-  int TPR, RPI, nLc, nSc, rows_per_chunk;       // element pass
+  int TPR, RPI, nLc, nSc, rows_per_chunk, Lc;   // element pass
   int nLt, nZt, nKc, dr_rows_per_chunk, rows_pad;  // dR GEMM
   int64_t ldg;                                  // G plane columns (3xf16, padded)
   size_t coef_bytes, colpart_bytes, slab_bytes, bound_bytes, planes_bytes;
@@ -1192,10 +1210,13 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   const int64_t dr_tile = planes ? dr16_tile(L, z) : 128;  // dR output tile edge
   pl.dr_tile = (int)dr_tile;
   pl.ldg = cdiv(L, dr_tile) * dr_tile;
-  // columns the element pass covers: with planes, L rounded up to the 32-wide
-  // K slices (zeros past L); the rest of the dR tile's padding is never
-  // written: in the dR GEMM it only meets output rows >= L, which are not stored
-  const int64_t Lc = planes ? std::min<int64_t>(pl.ldg, cdiv(L, 32) * 32) : L;
+  // columns the element pass covers: L rounded up to whole 4-column lane
+  // groups (the pad columns get G = 0).  The G planes' columns beyond are
+  // never written: in the dR GEMM a G column l meets only output row l, and
+  // rows >= L are not stored (round 5 wrote zeros up to the 32-wide chunk:
+  // L = 38 covered 64 columns, 40 now -- C2's element pass does 38 % less)
+  const int64_t Lc = planes ? std::min<int64_t>(pl.ldg, cdiv(L, 4) * 4) : L;
+  pl.Lc = (int)Lc;
   pl.nLc = (int)cdiv(Lc, 1024);
   pl.TPR = (int)(Lc >= 1024 ? 256 : cdiv(Lc, 4));
   pl.RPI = 256 / pl.TPR;
@@ -1298,7 +1319,6 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   float* colpart = reinterpret_cast<float*>(ws + pl.coef_bytes);
   float* slab = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes);
   float* gbound = reinterpret_cast<float*>(ws + pl.coef_bytes + pl.colpart_bytes + pl.slab_bytes);
-  float* gscale = gbound + shape->B;  // one float after the per-row bounds
   // G planes, chunked: rows_pad rows of gld = 2 * ldg halves
   uint16_t* g16 = reinterpret_cast<uint16_t*>(ws + pl.coef_bytes + pl.colpart_bytes +
                                               pl.slab_bytes + pl.bound_bytes);
@@ -1318,7 +1338,6 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
              a->c_coeff, a->live, kl, kl_blocks);
   if (int rc = check_launch("bwd_coef")) return rc;
   if (want_planes) {
-    if (int rc = launch_scale(gbound, B, gscale, st)) return rc;
     const int64_t pad_rows = (int64_t)pl.rows_pad - (int64_t)B * S;
     if (pad_rows > 0) {
       const size_t off = (size_t)B * S * gld, n = (size_t)pad_rows * gld * sizeof(uint16_t);
@@ -1336,14 +1355,14 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
   ep.coef = coef;
   ep.T = a->T;
   ep.g = want_planes ? g16 : nullptr;
-  ep.g_scale = gscale;
+  ep.g_bound = gbound;
   ep.gld = gld;
   ep.colpart = colpart;
   ep.S = S;
   ep.B = B;
   ep.L = L;
   ep.ldT = (int)t_cols(L);
-  ep.Lc = want_planes ? (int)std::min<int64_t>(pl.ldg, cdiv(L, 32) * 32) : L;
+  ep.Lc = want_planes ? pl.Lc : L;
   ep.TPR = pl.TPR;
   ep.RPI = pl.RPI;
   ep.rows_per_chunk = pl.rows_per_chunk;
@@ -1367,7 +1386,7 @@ int mpv_probit_bwd(const mpv_shape* shape, const mpv_bwd_args* a, void* stream) 
     if (planes) {
       Dr16Params dp;
       dp.g = g16;
-      dp.g_scale = gscale;
+      dp.g_bound = gbound;
       dp.gld = gld;
       dp.eps16 = a->eps16;
       dp.slab = slab;

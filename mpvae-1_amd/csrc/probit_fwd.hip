@@ -51,8 +51,13 @@ struct FwdParams {
 // 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3)
 constexpr int kCombineThreads = 1024;
 constexpr int kCombineFoldSlabs = 64;  // s-chunk partials fwd_combine sums itself, at most
+constexpr int kCombineKeep = 4;        // fwd_combine: samples per thread kept in registers
 constexpr int kFwdWant = 2048;         // fp32 mode: target workgroup count of the forward grid
 constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between scheduling barriers
+// samples per tile of the 48-label tile (L <= 48): 256 (C2 forward 25.1 us;
+// 128: 26.8; round 5's MFMA-layout 48 x 128 tile, two workgroups per CU
+// without packed fp32: 33.4; same box, eager)
+constexpr int kFwd48BM = 256;
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
@@ -991,13 +996,17 @@ MPV_DEV bool fwd_tile_soft(const FwdParams& p, int b, int n0, int nthreads) {
 // 128 samples for 48 < L <= 96: 8 waves of 48 labels x 32 samples), 2-stage
 // ring.  The waves of the second half issue the stage DMA at static priority 1
 // (the other half starts its MFMAs at the barrier).
-template <int WL, int WS, int TL, int TS, int NSTAGE>
+// LDS_MIN: the LDS size at least (one workgroup per CU whatever the register
+// count: packed fp32 VALU beside another workgroup's waves is not used, see
+// MPV_NO_PK_FP32).
+template <int WL, int WS, int TL, int TS, int NSTAGE, int LDS_MIN = 0>
 __global__ __launch_bounds__(WL* WS * 64, 8 / (WL * WS)) void probit_fwd16t_kernel(FwdParams p) {
   constexpr int NW = WL * WS;
   constexpr int BM = WS * TS * 16, BN = WL * TL * 16;  // samples, labels
   constexpr int STAGE = (BM + BN) * kRowB;
   constexpr int RED = WL * BM * 6, CACC = WS * BN * 2;  // floats
-  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (RED + CACC + kColsT * BN) * 4];
+  constexpr int LDS = NSTAGE * STAGE + (RED + CACC + kColsT * BN) * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS > LDS_MIN ? LDS : LDS_MIN];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   float* cacc = red + RED;
   float* cols = cacc + CACC;
@@ -1161,7 +1170,78 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
 }
 
+// The six scalars of compute_loss (mpvae.py:147-148 KL, :188-190 nll, :122
+// ranking mean, :207-208 total) from the per-row statistics, by ONE block of
+// kFinalThreads threads.  row(b, v) yields row b's (M, Z, M_x, Z_x, c, c_x);
+// both finalize variants sum in this same order.
+constexpr int kFinalThreads = 1024;
+template <class Row>
+MPV_DEV void finalize_scalars(const mpv_final_args& a, int B, float S_total, Row row) {
+  __shared__ float red[16 * 5];
+  const int tid = threadIdx.x;
+  float ne = 0.f, nx = 0.f, ce = 0.f, cx = 0.f;
+  for (int b = tid; b < B; b += blockDim.x) {
+    float v[6];
+    row(b, v);
+    // nll = mean_b(-log(mean_s exp(logp - max)) - max)   (mpvae.py:188-190)
+    ne += -logf(v[1] / S_total) - v[0];
+    nx += -logf(v[3] / S_total) - v[2];
+    ce += v[4];
+    cx += v[5];
+  }
+  float kl = 0.f;
+  const int64_t nd = (int64_t)B * a.d;
+  auto klt = [](float lve, float lvx, float mue, float mux) {
+    const float dm = mux - mue;
+    return (lvx - lve) - 1.0f + expf(lve - lvx) + dm * dm / (expf(lvx) + kKlEps);
+  };
+  const bool vec = (nd & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a.fe_logvar) | reinterpret_cast<uintptr_t>(a.fx_logvar) |
+                     reinterpret_cast<uintptr_t>(a.fe_mu) | reinterpret_cast<uintptr_t>(a.fx_mu)) & 15) == 0;
+  if (vec) {  // four elements per thread and pass, 16-B loads (one block does all of B x d:
+              // the scalar loop's dependent loads made this launch 20 us at C4)
+    for (int64_t i = 4 * (int64_t)tid; i < nd; i += 4 * (int64_t)blockDim.x) {
+      const f32x4 le = *reinterpret_cast<const f32x4*>(a.fe_logvar + i);
+      const f32x4 lx = *reinterpret_cast<const f32x4*>(a.fx_logvar + i);
+      const f32x4 me = *reinterpret_cast<const f32x4*>(a.fe_mu + i);
+      const f32x4 mx = *reinterpret_cast<const f32x4*>(a.fx_mu + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kl += klt(le[q], lx[q], me[q], mx[q]);
+    }
+  } else {
+#pragma unroll 4
+    for (int64_t i = tid; i < nd; i += blockDim.x)
+      kl += klt(a.fe_logvar[i], a.fx_logvar[i], a.fe_mu[i], a.fx_mu[i]);
+  }
+  float r5[5] = {ne, nx, ce, cx, kl};
+  block_reduce_n<5, false>(r5, red);  // one barrier pair; each value as block_reduce sums it
+  ne = r5[0], nx = r5[1], ce = r5[2], cx = r5[3], kl = r5[4];
+  if (tid == 0) {
+    const float nll = ne / (float)B, nll_x = nx / (float)B;
+    const float c = ce / (S_total * (float)B), c_x = cx / (S_total * (float)B);
+    const float klv = 0.5f * kl / (float)B;
+    *a.nll = nll;
+    *a.nll_x = nll_x;
+    *a.c = c;
+    *a.c_x = c_x;
+    *a.kl = klv;
+    // total (mpvae.py:207-208)
+    *a.total = (nll + nll_x) * a.nll_coeff + (c + c_x) * a.c_coeff + klv * kKlWeight;
+  }
+}
+
+// indiv_prob_label / indiv_prob (mpvae.py:203-204) of element i = b L + l
+MPV_DEV void write_indiv(const mpv_final_args& a, int64_t n, int64_t i, float e, float x,
+                         float S_total) {
+  a.indiv_prob_label[i] = e / S_total;
+  a.indiv_prob[i] = x / S_total;
+  (void)n;
+}
+
 // One block per batch row b.  rowpart -> rowstat, bstat.
+// (Round 6 measured the finalize folded into this kernel's last-arriving
+// block: the device-scope release fence each block then needs writes back its
+// XCD's L2, and the combine ran 13 -> 53 us at C2, 77 -> 270 us at C4.)
 __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const float* __restrict__ y,
                                                          const float* __restrict__ rowpart,
                                                          float* __restrict__ rowstat,
@@ -1169,7 +1249,7 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
                                                          int L, int nNt,
                                                          const float* __restrict__ colpart,
                                                          float* __restrict__ colsum, int nSc) {
-  __shared__ float red[32];
+  __shared__ float red[32], red2[32];
   const int b = blockIdx.x, tid = threadIdx.x;
   // this row's column sums over the s-chunks (colpart != NULL: the workgroups
   // of several s-chunks wrote partials), summed in chunk order
@@ -1193,7 +1273,10 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
   const float nrm = np * nn;  // normalizers = |pos| * |neg|  (mpvae.py:115-117)
 
   float me = -INFINITY, mx = -INFINITY, ce = 0.f, cx = 0.f;
-  for (int s = tid; s < S; s += blockDim.x) {
+  // the row's first kCombineKeep passes of log-probs stay in registers for the
+  // log-sum-exp pass (no second read of rowstat for S <= kCombineKeep * 1024)
+  float keep0[kCombineKeep], keep1[kCombineKeep];
+  auto sample = [&](int s, float& l0, float& l1) {
     float v[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -1209,11 +1292,47 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
     const float lx = (v[4] * v[5]) / (5.0f * nrm);
     ce += isfinite(le) ? le : 0.0f;
     cx += isfinite(lx) ? lx : 0.0f;
+    l0 = v[0];
+    l1 = v[1];
+  };
+#pragma unroll
+  for (int j = 0; j < kCombineKeep; ++j) {
+    const int s = tid + j * (int)blockDim.x;
+    if (s < S) sample(s, keep0[j], keep1[j]);
   }
-  block_reduce2<true>(me, mx, red);
-  block_reduce2<false>(ce, cx, red);
+  for (int s = tid + kCombineKeep * (int)blockDim.x; s < S; s += blockDim.x) {
+    float l0, l1;
+    sample(s, l0, l1);
+  }
+  {  // the two maxima and the two ranking sums with one barrier pair, each
+     // combined in block_reduce's order
+    const int lane = tid & 63, wid = tid >> 6, nw = (blockDim.x + 63) >> 6;
+    me = wave_max(me);
+    mx = wave_max(mx);
+    ce = wave_sum(ce);
+    cx = wave_sum(cx);
+    __syncthreads();
+    if (lane == 0) red[wid] = me, red[16 + wid] = mx, red2[wid] = ce, red2[16 + wid] = cx;
+    __syncthreads();
+    me = mx = -INFINITY;
+    ce = cx = 0.0f;
+    for (int i = 0; i < nw; ++i) {
+      me = fmaxf(me, red[i]);
+      mx = fmaxf(mx, red[16 + i]);
+      ce += red2[i];
+      cx += red2[16 + i];
+    }
+  }
   float ze = 0.f, zx = 0.f;
-  for (int s = tid; s < S; s += blockDim.x) {
+#pragma unroll
+  for (int j = 0; j < kCombineKeep; ++j) {
+    const int s = tid + j * (int)blockDim.x;
+    if (s < S) {
+      ze += expf(keep0[j] - me);
+      zx += expf(keep1[j] - mx);
+    }
+  }
+  for (int s = tid + kCombineKeep * (int)blockDim.x; s < S; s += blockDim.x) {
     ze += expf(rowstat[((int64_t)0 * B + b) * S + s] - me);
     zx += expf(rowstat[((int64_t)1 * B + b) * S + s] - mx);
   }
@@ -1229,52 +1348,33 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
 }
 
 // Block 0: the six scalars; blocks >= 1: indiv_prob / indiv_prob_label.
-__global__ __launch_bounds__(1024) void finalize_kernel(mpv_final_args a, int B, int L,
-                                                      float S_total) {
+// SLOTS (the sharded path): a.bstat is the all-reduced (nslots, 6, B) slot
+// buffer of the shards' statistics; block 0 combines each row exactly
+// (bstat_combine_row, as mpv_bstat_combine) into bstat_out for the backward
+// and finalizes from the combined values: one launch instead of two.
+template <bool SLOTS>
+__global__ __launch_bounds__(kFinalThreads) void finalize_kernel(mpv_final_args a, int B, int L,
+                                                               float S_total, int nslots,
+                                                               float* __restrict__ bstat_out) {
   if (blockIdx.x > 0) {
     const int64_t n = (int64_t)B * L;
     for (int64_t i = (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)(gridDim.x - 1) * blockDim.x) {
-      a.indiv_prob_label[i] = a.colsum[i] / S_total;
-      a.indiv_prob[i] = a.colsum[n + i] / S_total;
-    }
+         i += (int64_t)(gridDim.x - 1) * blockDim.x)
+      write_indiv(a, n, i, a.colsum[i], a.colsum[n + i], S_total);
     return;
   }
-  __shared__ float red[16];
-  const int tid = threadIdx.x;
-  float ne = 0.f, nx = 0.f, ce = 0.f, cx = 0.f;
-  for (int b = tid; b < B; b += blockDim.x) {
-    // nll = mean_b(-log(mean_s exp(logp - max)) - max)   (mpvae.py:188-190)
-    ne += -logf(a.bstat[1 * B + b] / S_total) - a.bstat[0 * B + b];
-    nx += -logf(a.bstat[3 * B + b] / S_total) - a.bstat[2 * B + b];
-    ce += a.bstat[4 * B + b];
-    cx += a.bstat[5 * B + b];
-  }
-  float kl = 0.f;
-  const int64_t nd = (int64_t)B * a.d;
-#pragma unroll 4
-  for (int64_t i = tid; i < nd; i += blockDim.x) {
-    const float lve = a.fe_logvar[i], lvx = a.fx_logvar[i];
-    const float dm = a.fx_mu[i] - a.fe_mu[i];
-    kl += (lvx - lve) - 1.0f + expf(lve - lvx) + dm * dm / (expf(lvx) + kKlEps);
-  }
-  ne = block_reduce<false>(ne, red);
-  nx = block_reduce<false>(nx, red);
-  ce = block_reduce<false>(ce, red);
-  cx = block_reduce<false>(cx, red);
-  kl = block_reduce<false>(kl, red);
-  if (tid == 0) {
-    const float nll = ne / (float)B, nll_x = nx / (float)B;
-    const float c = ce / (S_total * (float)B), c_x = cx / (S_total * (float)B);
-    const float klv = 0.5f * kl / (float)B;
-    *a.nll = nll;
-    *a.nll_x = nll_x;
-    *a.c = c;
-    *a.c_x = c_x;
-    *a.kl = klv;
-    // total (mpvae.py:207-208)
-    *a.total = (nll + nll_x) * a.nll_coeff + (c + c_x) * a.c_coeff + klv * kKlWeight;
-  }
+  // the step's noise has been drawn (stream order): advance its device key
+  if (a.seed_advance != nullptr && threadIdx.x == 0) *a.seed_advance += 1ull;
+  finalize_scalars(a, B, S_total, [&](int b, float (&v)[6]) {
+    if (SLOTS) {
+      bstat_combine_row(a.bstat, nslots, B, b, v);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) bstat_out[(int64_t)k * B + b] = v[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = a.bstat[(int64_t)k * B + b];
+    }
+  });
 }
 
 // ---------------------------------------------------------------- host side
@@ -1294,7 +1394,7 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   // transposed 96-label tile is the one used now.)
   const bool f16 = gemm == MPV_GEMM_F16X3;
   pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : ((f16 && s->L > 128) ? 3 : 2));
-  pl.BM = 128;
+  pl.BM = (f16 && pl.cfg == 0) ? kFwd48BM : 128;
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
@@ -1302,7 +1402,7 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   // per CU for the 48-label tile, 1 for the 8-wave tiles); longer runs per
   // workgroup amortize its prologue (C3 step 0.534 -> 0.510 ms against a
   // 2048-workgroup target, C2 the same; C4 has one s-chunk either way)
-  const int64_t target = f16 ? (pl.cfg == 0 ? 2 : 1) * (int64_t)num_cus() : kFwdWant;
+  const int64_t target = f16 ? (int64_t)num_cus() : kFwdWant;
   int64_t want = cdiv(target, s->B * (int64_t)pl.nNt);
   if (want < 1) want = 1;
   if (want > pl.nSt) want = pl.nSt;
@@ -1328,8 +1428,9 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
     }
   } else {
     switch (pl.cfg) {
-      case 0:  // BN 48, 4 waves, 3-stage ring (66 KB LDS: 2 workgroups per CU)
-        MPV_LAUNCH("probit_fwd", (probit_fwd16_kernel<4, 1, 2, 3, 3>), grid, dim3(256), 0, st, p);
+      case 0:  // 48 labels x kFwd48BM samples, transposed, 8 waves, one workgroup per CU
+        MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<1, 8, 3, kFwd48BM / 128, 2, 82 * 1024>), grid,
+                   dim3(512), 0, st, p);
         break;
       case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
         MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3, 4>), grid, dim3(512), 0, st, p);
@@ -1379,7 +1480,30 @@ size_t mpv_fwd_workspace_bytes(const mpv_shape* shape) {
   return most;
 }
 
-int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) {
+}  // extern "C"
+
+namespace mpv {
+
+static int check_final_args(const mpv_final_args* a, bool need_stats) {
+  MPV_REQUIRE(a && (!need_stats || (a->bstat && a->colsum)) && a->fe_mu && a->fe_logvar &&
+                  a->fx_mu && a->fx_logvar && a->total && a->nll && a->nll_x && a->c && a->c_x &&
+                  a->kl && a->indiv_prob && a->indiv_prob_label && a->d > 0,
+              "NULL pointer in mpv_final_args");
+  return MPV_OK;
+}
+
+template <bool SLOTS>
+static int launch_finalize(const mpv_shape* shape, const mpv_final_args& a, int nslots,
+                           float* bstat_out, hipStream_t st) {
+  const int64_t n = shape->B * shape->L;
+  int64_t nb = cdiv(n, 1024);
+  if (nb > 2048) nb = 2048;
+  MPV_LAUNCH("finalize", finalize_kernel<SLOTS>, dim3((unsigned)(1 + nb)), dim3(kFinalThreads), 0,
+             st, a, (int)shape->B, (int)shape->L, (float)shape->S_total, nslots, bstat_out);
+  return check_launch("finalize");
+}
+
+static int run_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) {
   if (int rc = check_shape(shape)) return rc;
   MPV_REQUIRE(a != nullptr, "args is NULL");
   MPV_REQUIRE(a->y && a->fe_out && a->fx_out && a->rowstat && a->bstat && a->colsum &&
@@ -1399,9 +1523,9 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
                     (int64_t)pl.BN * a->R16.ld * 2 < (int64_t(1) << 32),
                 "ld too large for the f16x3 tile offsets");
   }
-  MPV_REQUIRE(a->workspace_bytes >= pl.rowpart_bytes + pl.colpart_bytes,
-              "workspace too small: %zu < %zu", a->workspace_bytes,
-              pl.rowpart_bytes + pl.colpart_bytes);
+  const size_t need = pl.rowpart_bytes + pl.colpart_bytes;
+  MPV_REQUIRE(a->workspace_bytes >= need, "workspace too small: %zu < %zu", a->workspace_bytes,
+              need);
   hipStream_t st = as_stream(stream);
   FwdParams p;
   p.y = a->y;
@@ -1431,9 +1555,9 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   // few s-chunks: fwd_combine sums the column partials too (one launch less);
   // many (small B, long S): the slab-sum kernel's split reduction
   const bool fold = pl.nSc > 1 && pl.nSc <= kCombineFoldSlabs;
-  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(kCombineThreads), 0, st, a->y,
-             p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt, fold ? p.colpart : nullptr,
-             a->colsum, pl.nSc);
+  MPV_LAUNCH("fwd_combine", fwd_combine_kernel, dim3((unsigned)shape->B), dim3(kCombineThreads), 0,
+             st, a->y, p.rowpart, a->rowstat, a->bstat, p.S, p.B, p.L, pl.nNt,
+             fold ? p.colpart : nullptr, a->colsum, pl.nSc);
   if (int rc = check_launch("fwd_combine")) return rc;
   if (pl.nSc > 1 && !fold) {
     if (int rc = launch_sum_slabs(p.colpart, pl.nSc, 2 * shape->B * shape->L, a->colsum, MPV_F32, st))
@@ -1442,18 +1566,30 @@ int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) 
   return MPV_OK;
 }
 
+}  // namespace mpv
+
+extern "C" {
+
+int mpv_probit_fwd(const mpv_shape* shape, const mpv_fwd_args* a, void* stream) {
+  return run_fwd(shape, a, stream);
+}
+
 int mpv_probit_finalize(const mpv_shape* shape, const mpv_final_args* a, void* stream) {
   MPV_REQUIRE(shape && shape->B > 0 && shape->L > 0 && shape->S_total > 0, "bad shape");
-  MPV_REQUIRE(a && a->bstat && a->colsum && a->fe_mu && a->fe_logvar && a->fx_mu &&
-                  a->fx_logvar && a->total && a->nll && a->nll_x && a->c && a->c_x && a->kl &&
-                  a->indiv_prob && a->indiv_prob_label && a->d > 0,
-              "NULL pointer in mpv_final_args");
-  const int64_t n = shape->B * shape->L;
-  int64_t nb = cdiv(n, 1024);
-  if (nb > 2048) nb = 2048;
-  MPV_LAUNCH("finalize", finalize_kernel, dim3((unsigned)(1 + nb)), dim3(1024), 0,
-             as_stream(stream), *a, (int)shape->B, (int)shape->L, (float)shape->S_total);
-  return check_launch("finalize");
+  if (int rc = check_final_args(a, true)) return rc;
+  return launch_finalize<false>(shape, *a, 0, nullptr, as_stream(stream));
+}
+
+int mpv_probit_finalize_shards(const mpv_shape* shape, const float* slots, int64_t nslots,
+                               float* bstat_out, const mpv_final_args* a, void* stream) {
+  MPV_REQUIRE(shape && shape->B > 0 && shape->L > 0 && shape->S_total > 0, "bad shape");
+  MPV_REQUIRE(slots && bstat_out && nslots > 0 && nslots < (int64_t(1) << 20),
+              "bad slot arguments");
+  if (int rc = check_final_args(a, false)) return rc;
+  MPV_REQUIRE(a->colsum != nullptr, "colsum is NULL");
+  mpv_final_args f = *a;
+  f.bstat = slots;  // (nslots, 6, B), combined row by row in the kernel
+  return launch_finalize<true>(shape, f, (int)nslots, bstat_out, as_stream(stream));
 }
 
 }  // extern "C"

@@ -237,22 +237,10 @@ __global__ void bstat_combine_kernel(const float* __restrict__ g, int64_t R, int
                                      float* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  float v[6];
+  bstat_combine_row(g, R, B, b, v);
 #pragma unroll
-  for (int br = 0; br < 2; ++br) {
-    const int mi = 2 * br, zi = 2 * br + 1;
-    float M = -INFINITY;
-    for (int64_t r = 0; r < R; ++r) M = fmaxf(M, g[(r * 6 + mi) * B + b]);
-    float Z = 0.0f;
-    for (int64_t r = 0; r < R; ++r)
-      Z += g[(r * 6 + zi) * B + b] * expf(g[(r * 6 + mi) * B + b] - M);
-    out[mi * B + b] = M;
-    out[zi * B + b] = Z;
-  }
-  for (int k = 4; k < 6; ++k) {
-    float acc = 0.0f;
-    for (int64_t r = 0; r < R; ++r) acc += g[(r * 6 + k) * B + b];
-    out[k * B + b] = acc;
-  }
+  for (int k = 0; k < 6; ++k) out[k * B + b] = v[k];
 }
 
 // ------------------------------------------------------ reparameterisation
@@ -305,7 +293,8 @@ __global__ void kl_bwd_kernel(mpv_kl_bwd_args a) {
 }
 
 // --------------------------------------------------------- 3xf16 operands
-constexpr int kMaxBlocks = 1024;  // block maxima of maxabs_kernel
+constexpr int kMaxBlocks = 1024;  // block maxima of maxabs_kernel (workspace size)
+constexpr int kSplitMaxBlocks = 256;  // maxabs blocks of mpv_split_f16 (read by every split wave)
 
 template <typename T>
 __global__ __launch_bounds__(256) void maxabs_kernel(const T* __restrict__ x, int64_t n,
@@ -319,22 +308,18 @@ __global__ __launch_bounds__(256) void maxabs_kernel(const T* __restrict__ x, in
   if (threadIdx.x == 0) block_max[blockIdx.x] = m;
 }
 
-// scale = pow2_scale(max of n block maxima) [* extra bound factor]
-__global__ __launch_bounds__(256) void scale_kernel(const float* __restrict__ block_max, int n,
-                                                   float* __restrict__ scale) {
-  __shared__ float red[16];
-  float m = 0.0f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, block_max[i]);
-  m = block_reduce<true>(m, red);
-  if (threadIdx.x == 0) *scale = pow2_scale(m);
-}
 
 // (rows, cols) row-major -> chunked split planes (rows_pad x ld/2 columns),
 // zero padded.  Thread i owns logical element (r, c) = (i / cols_pad, i % cols_pad).
+// The scale comes from the nb block maxima of maxabs_kernel, taken by every
+// wave itself (wave_pow2_scale: the same bits as a scale launch of its own,
+// one launch fewer); block 0 publishes it.
 template <typename T>
 __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int64_t rows,
-                                                   int64_t cols, mpv_split16 out) {
-  const float s = *out.scale;
+                                                   int64_t cols, mpv_split16 out,
+                                                   const float* __restrict__ bmax, int nb) {
+  const float s = wave_pow2_scale(bmax, nb);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = s;
   const int64_t cp = out.ld >> 1;
   const int64_t n = out.rows_pad * cp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -355,17 +340,29 @@ __global__ __launch_bounds__(256) void split_kernel(const T* __restrict__ x, int
 // same scale bits in every workgroup (the max is exact in any order).
 constexpr int64_t kSplitSmall = 16384;  // input elements
 
+// (block `blk` of `nblk` doing this split; split_small_kernel's whole grid, or
+// the extra workgroups of noise_philox16_kernel, mpv_noise_philox_f16_split)
 template <typename T>
-__global__ __launch_bounds__(256) void split_small_kernel(const T* __restrict__ x, int rows,
-                                                         int cols, mpv_split16 out) {
+MPV_DEV void split_small_body(const T* __restrict__ x, int rows, int cols, const mpv_split16& out,
+                              int blk, int nblk) {
   __shared__ float red[16];
-  const int n = rows * cols;
-  float m = 0.0f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf((float)x[i]));
+  const int n = rows * cols, st = blockDim.x;
+  // four independent chains (the loads in flight together; a max is exact in
+  // any order)
+  float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
+  int i = threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    m0 = fmaxf(m0, fabsf((float)x[i]));
+    m1 = fmaxf(m1, fabsf((float)x[i + st]));
+    m2 = fmaxf(m2, fabsf((float)x[i + 2 * st]));
+    m3 = fmaxf(m3, fabsf((float)x[i + 3 * st]));
+  }
+  for (; i < n; i += st) m0 = fmaxf(m0, fabsf((float)x[i]));
+  const float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
   const float s = pow2_scale(block_reduce<true>(m, red));
-  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = s;
+  if (blk == 0 && threadIdx.x == 0) *out.scale = s;
   const int cp = (int)(out.ld >> 1), np = (int)out.rows_pad * cp;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < np; i += gridDim.x * blockDim.x) {
+  for (int i = blk * blockDim.x + threadIdx.x; i < np; i += nblk * blockDim.x) {
     const int r = i / cp, c = i - r * cp;
     const float v = (r < rows && c < cols) ? (float)x[r * cols + c] : 0.0f;
     uint16_t h, l;
@@ -375,6 +372,20 @@ __global__ __launch_bounds__(256) void split_small_kernel(const T* __restrict__ 
     out.data[o + kLoOff] = l;
   }
 }
+
+template <typename T>
+__global__ __launch_bounds__(256) void split_small_kernel(const T* __restrict__ x, int rows,
+                                                         int cols, mpv_split16 out) {
+  split_small_body<T>(x, rows, cols, out, blockIdx.x, gridDim.x);
+}
+
+// A small operand split riding on the noise launch (mpv_noise_philox_f16_split).
+struct SmallSplit {
+  const void* x;
+  int f64, rows, cols;
+  mpv_split16 out;
+  int nblocks;  // the grid's last nblocks workgroups split; 0: none
+};
 
 // Philox noise straight into 3xf16 planes: plane row r = b*S_local + s holds
 // the noise of (s, b) (same values as the fp32 (S, B, z) draw, rows reordered
@@ -478,23 +489,36 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
                                                             int z, int64_t s_off, uint32_t k0,
                                                             uint32_t k1, uint64_t offset,
                                                             int rows,
-                                                            const uint64_t* __restrict__ seed_dev) {
+                                                            const uint64_t* __restrict__ seed_dev,
+                                                            SmallSplit ss) {
+  // r_sqrt_sigma's split, beside the noise (one launch): the first workgroups,
+  // so that they start with the noise's and finish under it
+  if ((int)blockIdx.x < ss.nblocks) {
+    if (ss.f64)
+      split_small_body<double>((const double*)ss.x, ss.rows, ss.cols, ss.out, blockIdx.x,
+                               ss.nblocks);
+    else
+      split_small_body<float>((const float*)ss.x, ss.rows, ss.cols, ss.out, blockIdx.x,
+                              ss.nblocks);
+    return;
+  }
+  const int nblk = (int)blockIdx.x - ss.nblocks;  // this workgroup's noise block
   philox_key(seed_dev, k0, k1);
   // the planes' constant scale (no launch of its own; the GEMMs that read it
   // run after this kernel)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = kNoiseScale;
+  if (nblk == 0 && threadIdx.x == 0) *out.scale = kNoiseScale;
   const int cols = noise_written_cols(out, z);
-  const int r_end = min(rows, (int)(blockIdx.x + 1) * kNoiseRows);
+  const int r_end = min(rows, (int)(nblk + 1) * kNoiseRows);
   constexpr int CPT = kNoiseCols;
   const int tpr = min((int)blockDim.x, cols / CPT);  // threads per row
   if (tpr == (int)blockDim.x) {  // wide planes: the row (and its index math) is block-uniform
-    for (int r = blockIdx.x * kNoiseRows; r < r_end; ++r)
+    for (int r = nblk * kNoiseRows; r < r_end; ++r)
       noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, threadIdx.x * CPT,
                        blockDim.x * CPT);
   } else {  // narrow planes (C2, C3): several rows per pass of the block
     const int rpi = (int)blockDim.x / tpr;
     if ((int)threadIdx.x >= rpi * tpr) return;
-    for (int r = blockIdx.x * kNoiseRows + (int)threadIdx.x / tpr; r < r_end; r += rpi)
+    for (int r = nblk * kNoiseRows + (int)threadIdx.x / tpr; r < r_end; r += rpi)
       noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, ((int)threadIdx.x % tpr) * CPT,
                        tpr * CPT);
   }
@@ -613,24 +637,24 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
   }
   float* bmax = reinterpret_cast<float*>(workspace);
   const int64_t n = rows * cols;
-  const unsigned g = grid_for(n, 256, kMaxBlocks);
+  const unsigned g = grid_for(n, 256, kSplitMaxBlocks);
   if (x_dtype == MPV_F64)
     MPV_LAUNCH("split", maxabs_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)x, n, bmax);
   else
     MPV_LAUNCH("split", maxabs_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, n, bmax);
-  MPV_LAUNCH("split", scale_kernel, dim3(1), dim3(256), 0, s, bmax, (int)g, out->scale);
   const unsigned g2 = grid_for(out->rows_pad * (out->ld / 2), 256, 16384);
   if (x_dtype == MPV_F64)
     MPV_LAUNCH("split", split_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)x, rows,
-               cols, *out);
+               cols, *out, bmax, (int)g);
   else
     MPV_LAUNCH("split", split_kernel<float>, dim3(g2), dim3(256), 0, s, (const float*)x, rows,
-               cols, *out);
+               cols, *out, bmax, (int)g);
   return check_launch("split_f16");
 }
 
 static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_t* seed_dev,
-                            uint64_t offset, const mpv_split16* out, void* stream) {
+                            uint64_t offset, const mpv_split16* out, void* stream,
+                            SmallSplit ss = SmallSplit{}) {
   if (int rc = check_shape(shape)) return rc;
   if (int rc = check_split(out)) return rc;
   const int64_t rows = shape->S_local * shape->B;
@@ -639,9 +663,15 @@ static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_
   MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
   const int64_t tpr = noise_written_cols(*out, (int)shape->z) / kNoiseCols;  // threads per plane row
   const unsigned threads = tpr >= 256 ? 256 : (unsigned)(cdiv(tpr, 64) * 64);
-  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)cdiv(rows, kNoiseRows)),
-             dim3(threads), 0, s, *out, (int)shape->S_local, (int)shape->B, (int)shape->z,
-             shape->s_offset, (uint32_t)seed, (uint32_t)(seed >> 32), offset, (int)rows, seed_dev);
+  if (ss.x != nullptr) {
+    const int64_t plane_elems = ss.out.rows_pad * (ss.out.ld / 2);
+    ss.nblocks = (int)std::min<int64_t>(cdiv(plane_elems, (int64_t)threads * 8), 64);
+  }
+  const int64_t nb = cdiv(rows, kNoiseRows) + ss.nblocks;
+  MPV_REQUIRE(nb < (int64_t(1) << 31), "noise grid too large");
+  MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)nb), dim3(threads), 0, s, *out,
+             (int)shape->S_local, (int)shape->B, (int)shape->z, shape->s_offset, (uint32_t)seed,
+             (uint32_t)(seed >> 32), offset, (int)rows, seed_dev, ss);
   return check_launch("noise_philox_f16");
 }
 
@@ -654,6 +684,21 @@ int mpv_noise_philox_f16_dev(const mpv_shape* shape, const uint64_t* seed_dev, u
                              const mpv_split16* out, void* stream) {
   MPV_REQUIRE(seed_dev != nullptr, "seed_dev is NULL");
   return noise_philox_f16(shape, 0, seed_dev, offset, out, stream);
+}
+
+int mpv_noise_philox_f16_split(const mpv_shape* shape, uint64_t seed, const uint64_t* seed_dev,
+                               uint64_t offset, const mpv_split16* out, const void* x,
+                               int x_dtype, int64_t rows, int64_t cols,
+                               const mpv_split16* x_out, void* stream) {
+  if (int rc = check_split(x_out)) return rc;
+  MPV_REQUIRE(x && rows > 0 && cols > 0 && rows * cols <= kSplitSmall,
+              "the split rides on the noise launch for at most %lld elements",
+              (long long)kSplitSmall);
+  MPV_REQUIRE(rows <= x_out->rows_pad && cols <= x_out->ld / 2, "planes smaller than the input");
+  MPV_REQUIRE(x_out->rows_pad * (x_out->ld / 2) < (int64_t(1) << 31), "planes too large");
+  MPV_REQUIRE(x_dtype == MPV_F32 || x_dtype == MPV_F64, "unsupported dtype %d", x_dtype);
+  SmallSplit ss{x, x_dtype == MPV_F64, (int)rows, (int)cols, *x_out, 0};
+  return noise_philox_f16(shape, seed, seed_dev, offset, out, stream, ss);
 }
 
 int mpv_convert(const void* src, int sd, void* dst, int dd, int64_t n, void* stream) {
@@ -724,10 +769,6 @@ int mpv_kl_bwd(const mpv_kl_bwd_args* a, void* stream) {
 
 namespace mpv {
 // Used by the forward / backward translation units.
-int launch_scale(const float* block_max, int n, float* scale, hipStream_t s) {
-  MPV_LAUNCH("bwd_coef", scale_kernel, dim3(1), dim3(256), 0, s, block_max, n, scale);
-  return check_launch("scale");
-}
 
 static SlabSum slab_problem(const float* in, int64_t nslab, int64_t n, void* out, int out_dtype) {
   SlabSum q;

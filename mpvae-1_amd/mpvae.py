@@ -239,10 +239,18 @@ def _noise_source(args, n_sample, B, z, shard, device):
     if mode == "philox":
         # args.mpvae_seed: an int, or a one-element int64 tensor on the device
         # whose value the noise kernel reads at run time (no host sync; a step
-        # captured in a HIP graph draws fresh noise when the tensor advances)
+        # captured in a HIP graph draws fresh noise when the tensor advances).
+        # args.mpvae_seed_advance (with a device tensor): the finalize launch
+        # advances it by 1 once this step's noise has read it, so the next call
+        # (or graph replay) draws fresh noise with no launch of its own
         seed = getattr(args, "mpvae_seed", None)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        advance = seed if (getattr(args, "mpvae_seed_advance", False)
+                           and isinstance(seed, torch.Tensor)) else None
+        if getattr(args, "mpvae_seed_advance", False) and advance is None:
+            raise ValueError("args.mpvae_seed_advance needs args.mpvae_seed to be a one-element "
+                             "int64 device tensor")
         if shard.exchange is not None:
             # one noise stream for the whole job: rank 0's seed (mpvae_dist.py).
             # An int key travels as a device tensor written by a fill kernel (no
@@ -254,7 +262,7 @@ def _noise_source(args, n_sample, B, z, shard, device):
                 seed = torch.full((1,), u - 2 ** 64 if u >= 2 ** 63 else u, dtype=torch.int64,
                                   device=device)
             seed = shard.exchange.agree_seed(seed, device)
-        return None, dict(noise="philox", seed=seed, offset=0)
+        return None, dict(noise="philox", seed=seed, offset=0, seed_advance=advance)
     raise ValueError(f"unknown args.mpvae_noise {mode!r} (torch_cpu | philox | tensor)")
 
 

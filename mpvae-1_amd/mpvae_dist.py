@@ -183,6 +183,19 @@ class SampleShardExchange:
                        lambda: dist.all_reduce(colsum, group=self.group))
         return bstat_global, colsum
 
+    def gather_slots(self, loc):
+        """The all-reduced packed buffer as (world, 6, B) bstat slots and the
+        summed colsum, for a backend that combines the slots inside its
+        finalize launch (HipShardBackend.finalize_slots); None without a
+        packed buffer (then combine() is used)."""
+        bstat, colsum, packed = loc["bstat"], loc["colsum"], loc.get("packed")
+        if packed is None:
+            return None
+        COMM_TIMER.run("combine_all_reduce", packed.device,
+                       lambda: dist.all_reduce(packed, group=self.group))
+        B = bstat.shape[1]
+        return packed[colsum.numel():].view(self.world, 6, B), colsum
+
     def reduce_grads(self, flat):
         COMM_TIMER.run("reduce_grads", flat.device, lambda: dist.all_reduce(flat, group=self.group))
         return flat

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (must precede the .so load: one HIP runtime per proc
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MPVAE_HIP_LIB", os.path.join(HERE, "libmpvae_hip.so"))
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 F32, F64 = 0, 1
 G_TOTAL, G_NLL, G_NLL_X, G_C, G_C_X, G_KL = range(6)
 
@@ -52,7 +52,7 @@ class FinalArgs(ctypes.Structure):
                 ("fx_logvar", vp), ("d", ctypes.c_int64), ("nll_coeff", ctypes.c_float),
                 ("c_coeff", ctypes.c_float), ("total", vp), ("nll", vp), ("nll_x", vp),
                 ("c", vp), ("c_x", vp), ("kl", vp), ("indiv_prob", vp),
-                ("indiv_prob_label", vp)]
+                ("indiv_prob_label", vp), ("seed_advance", vp)]
 
 
 class BwdArgs(ctypes.Structure):
@@ -68,7 +68,7 @@ class BwdArgs(ctypes.Structure):
 class KlBwdArgs(ctypes.Structure):
     _fields_ = [("fe_mu", vp), ("fe_logvar", vp), ("fx_mu", vp), ("fx_logvar", vp),
                 ("B", ctypes.c_int64), ("d", ctypes.c_int64), ("gscal", vp), ("g_fe_mu", vp),
-                ("g_fe_logvar", vp), ("g_fx_mu", vp), ("g_fx_logvar", vp)]
+                ("g_fe_logvar", vp), ("g_fx_mu", vp), ("g_fx_logvar", vp), ("live", ctypes.c_int)]
 
 
 class ReparamArgs(ctypes.Structure):
@@ -155,10 +155,16 @@ SIGNATURES = {
     "mpv_noise_philox_dev": (ctypes.c_int, [vp, ctypes.POINTER(Shape), vp, ctypes.c_uint64, vp]),
     "mpv_noise_philox_f16_dev": (ctypes.c_int, [ctypes.POINTER(Shape), vp, ctypes.c_uint64,
                                                 ctypes.POINTER(Split16), vp]),
+    "mpv_noise_philox_f16_split": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.c_uint64, vp,
+                                                  ctypes.c_uint64, ctypes.POINTER(Split16), vp,
+                                                  ctypes.c_int, ctypes.c_int64, ctypes.c_int64,
+                                                  ctypes.POINTER(Split16), vp]),
     "mpv_fwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape)]),
     "mpv_probit_fwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FwdArgs), vp]),
     "mpv_bstat_combine": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.c_int64, vp, vp]),
     "mpv_probit_finalize": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(FinalArgs), vp]),
+    "mpv_probit_finalize_shards": (ctypes.c_int, [ctypes.POINTER(Shape), vp, ctypes.c_int64, vp,
+                                                  ctypes.POINTER(FinalArgs), vp]),
     "mpv_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(Shape), ctypes.c_int]),
     "mpv_probit_bwd": (ctypes.c_int, [ctypes.POINTER(Shape), ctypes.POINTER(BwdArgs), vp]),
     "mpv_kl_bwd": (ctypes.c_int, [ctypes.POINTER(KlBwdArgs), vp]),

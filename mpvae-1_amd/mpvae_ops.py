@@ -78,6 +78,9 @@ class HipShardBackend:
     NaN instead of hiding behind the identical bytes the caching allocator
     hands back from an earlier launch."""
 
+    # the kernels read only the live upstream-gradient slots (ABI 10)
+    reads_live_slots = True
+
     def __init__(self, gemm="f16x3", poison=False):
         if gemm not in GEMMS:
             raise ValueError(f"gemm must be one of {sorted(GEMMS)} (got {gemm!r})")
@@ -93,16 +96,20 @@ class HipShardBackend:
     def shape(self, S_local, S_total, s_offset, B, L, z):
         return H.Shape(S_local, S_total, s_offset, B, L, z)
 
+    @staticmethod
+    def _check_seed(seed, device):
+        if isinstance(seed, torch.Tensor) and (seed.dtype != torch.int64 or seed.numel() != 1 or
+                                               seed.device != torch.device(device)):
+            raise ValueError("a device Philox seed must be a one-element int64 tensor on "
+                             f"{device} (got {seed.dtype}, {seed.numel()} elements, {seed.device})")
+
     def make_noise(self, shape, device, seed, offset):
         """Philox noise for this shard.  seed: an int (the key, passed by value)
         or a one-element int64 device tensor holding it (read by the kernel at
         run time: graph-capturable, no host sync)."""
         lib, st = H.load_library(), H.stream_of(device)
         dev_key = isinstance(seed, torch.Tensor)
-        if dev_key and (seed.dtype != torch.int64 or seed.numel() != 1 or
-                        seed.device != torch.device(device)):
-            raise ValueError("a device Philox seed must be a one-element int64 tensor on "
-                             f"{device} (got {seed.dtype}, {seed.numel()} elements, {seed.device})")
+        self._check_seed(seed, device)
         if self.gemm == H.GEMM_F16X3:
             eps = Planes(shape.S_local * shape.B, eps_cols(shape), device)
             if dev_key:
@@ -119,6 +126,29 @@ class HipShardBackend:
         else:
             H.check(lib.mpv_noise_philox(H.ptr(eps), shape, seed, offset, st), "mpv_noise_philox")
         return eps
+
+    # r_sqrt_sigma of at most this many elements is split inside the noise
+    # launch (mpv_noise_philox_f16_split; the split_small path)
+    SPLIT_WITH_NOISE = 16384
+
+    def make_noise_and_R(self, shape, device, seed, offset, R):
+        """(make_noise(...), prepare_R(R)) -- in ONE launch when the noise is
+        3xf16 Philox and R is small (L, z <= 128: C2, C3), else two."""
+        L, z = R.shape
+        if (self.gemm != H.GEMM_F16X3 or L * z > self.SPLIT_WITH_NOISE
+                or R.dtype not in (torch.float32, torch.float64)):
+            return self.make_noise(shape, device, seed, offset), self.prepare_R(R)
+        lib, st = H.load_library(), H.stream_of(device)
+        dev_key = isinstance(seed, torch.Tensor)
+        self._check_seed(seed, device)
+        eps = Planes(shape.S_local * shape.B, eps_cols(shape), device)
+        Rc = R.detach().contiguous()
+        Rop = Planes(_pad(L, 256), _pad(z, 128), R.device)
+        H.check(lib.mpv_noise_philox_f16_split(
+            shape, 0 if dev_key else int(seed) & (2 ** 64 - 1), H.ptr(seed) if dev_key else None,
+            offset, eps.c(), H.ptr(Rc), H.F64 if Rc.dtype == torch.float64 else H.F32, L, z,
+            Rop.c(), st), "mpv_noise_philox_f16_split")
+        return eps, Rop
 
     def _split(self, x, rows, cols, planes):
         lib = H.load_library()
@@ -201,6 +231,35 @@ class HipShardBackend:
         H.check(lib.mpv_probit_fwd(shape, args, H.stream_of(dev)), "mpv_probit_fwd")
         return dict(rowstat=rowstat, bstat=bstat, colsum=colsum, T=T, packed=packed)
 
+    def _final_args(self, shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar, nll_coeff,
+                    c_coeff, seed_advance=None):
+        dev = fe_mu.device
+        B, L = shape.B, shape.L
+        scal = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(6)]
+        indiv = torch.empty((B, L), device=dev, dtype=torch.float32)
+        indiv_label = torch.empty((B, L), device=dev, dtype=torch.float32)
+        args = H.FinalArgs(H.ptr(bstat), H.ptr(colsum), H.ptr(fe_mu), H.ptr(fe_logvar),
+                           H.ptr(fx_mu), H.ptr(fx_logvar), fe_mu.shape[1], nll_coeff, c_coeff,
+                           *[H.ptr(s) for s in scal], H.ptr(indiv), H.ptr(indiv_label),
+                           H.ptr(seed_advance))
+        return args, (*scal, indiv, indiv_label)
+
+    def finalize_slots(self, shape, slots, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar, nll_coeff,
+                       c_coeff, seed_advance=None):
+        """combine_bstats + finalize in one launch (mpv_probit_finalize_shards):
+        slots is the all-reduced (world, 6, B) buffer of the shards' bstat.
+        Returns (the combined (6, B) bstat, the 8 outputs)."""
+        B = shape.B
+        bstat = torch.empty((6, B), device=colsum.device, dtype=torch.float32)
+        fin, outs = self._final_args(shape, None, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
+                                     nll_coeff, c_coeff, seed_advance)
+        slots = slots.contiguous()
+        H.check(H.load_library().mpv_probit_finalize_shards(shape, H.ptr(slots), slots.shape[0],
+                                                             H.ptr(bstat), fin,
+                                                             H.stream_of(colsum.device)),
+                "mpv_probit_finalize_shards")
+        return bstat, outs
+
     def combine_bstats(self, gathered):
         R, _, B = gathered.shape
         out = torch.empty((6, B), device=gathered.device, dtype=torch.float32)
@@ -210,18 +269,14 @@ class HipShardBackend:
         return out
 
     def finalize(self, shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar, nll_coeff,
-                 c_coeff):
-        dev = bstat.device
-        B, L = shape.B, shape.L
-        scal = [torch.empty((), device=dev, dtype=torch.float32) for _ in range(6)]
-        indiv = torch.empty((B, L), device=dev, dtype=torch.float32)
-        indiv_label = torch.empty((B, L), device=dev, dtype=torch.float32)
-        args = H.FinalArgs(H.ptr(bstat), H.ptr(colsum), H.ptr(fe_mu), H.ptr(fe_logvar),
-                           H.ptr(fx_mu), H.ptr(fx_logvar), fe_mu.shape[1], nll_coeff, c_coeff,
-                           *[H.ptr(s) for s in scal], H.ptr(indiv), H.ptr(indiv_label))
-        H.check(H.load_library().mpv_probit_finalize(shape, args, H.stream_of(dev)),
+                 c_coeff, seed_advance=None):
+        """The 8 outputs; seed_advance: a device Philox key (int64 tensor) this
+        step's noise has read, advanced by 1 in the same launch."""
+        args, outs = self._final_args(shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
+                                      nll_coeff, c_coeff, seed_advance)
+        H.check(H.load_library().mpv_probit_finalize(shape, args, H.stream_of(bstat.device)),
                 "mpv_probit_finalize")
-        return (*scal, indiv, indiv_label)
+        return outs
 
     def backward_local(self, shape, saved, gscal, live, g_I, g_IL, nll_coeff, c_coeff, want_dR,
                        dR_dtype=torch.float32, kl=False):
@@ -247,7 +302,7 @@ class HipShardBackend:
         kl_outs, kl_ref = None, None
         if kl:
             kl_args, kl_outs = self._kl_args(saved["fe_mu"], saved["fe_logvar"], saved["fx_mu"],
-                                             saved["fx_logvar"], gscal)
+                                             saved["fx_logvar"], gscal, live)
             kl_ref = ctypes.byref(kl_args)
         args = H.BwdArgs(H.ptr(saved["y"]), H.ptr(saved["fe_out"]), H.ptr(saved["fx_out"]),
                          self.gemm, *eps_ops, H.ptr(saved["T"]), H.ptr(saved["rowstat"]),
@@ -261,15 +316,15 @@ class HipShardBackend:
         return flat, dfe_dfx, dR
 
     @staticmethod
-    def _kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
+    def _kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal, live=0x3F):
         B, d = fe_mu.shape
         outs = [torch.empty_like(fe_mu) for _ in range(4)]
         args = H.KlBwdArgs(H.ptr(fe_mu), H.ptr(fe_logvar), H.ptr(fx_mu), H.ptr(fx_logvar), B, d,
-                           H.ptr(gscal), *[H.ptr(o) for o in outs])
+                           H.ptr(gscal), *[H.ptr(o) for o in outs], live)
         return args, outs  # outs: g_fe_mu, g_fe_logvar, g_fx_mu, g_fx_logvar
 
-    def kl_backward(self, fe_mu, fe_logvar, fx_mu, fx_logvar, gscal):
-        args, outs = self._kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal)
+    def kl_backward(self, fe_mu, fe_logvar, fx_mu, fx_logvar, gscal, live=0x3F):
+        args, outs = self._kl_args(fe_mu, fe_logvar, fx_mu, fx_logvar, gscal, live)
         H.check(H.load_library().mpv_kl_bwd(args, H.stream_of(fe_mu.device)), "mpv_kl_bwd")
         return outs
 
@@ -295,13 +350,16 @@ class ElboConfig:
     """Non-tensor arguments of ProbitELBO."""
 
     def __init__(self, S_total, S_local, s_offset, nll_coeff, c_coeff, noise="explicit",
-                 seed=0, offset=0, backend=None, exchange=None, gemm="f16x3"):
+                 seed=0, offset=0, backend=None, exchange=None, gemm="f16x3", seed_advance=None):
         self.S_total, self.S_local, self.s_offset = int(S_total), int(S_local), int(s_offset)
         self.nll_coeff, self.c_coeff = float(nll_coeff), float(c_coeff)
         # seed: an int, or a one-element int64 device tensor (HipShardBackend.make_noise)
         self.noise, self.offset = noise, int(offset)
         self.seed = seed if isinstance(seed, torch.Tensor) else int(seed)
         self.backend = backend if backend is not None else HipShardBackend(gemm)
+        # a device int64 key tensor the finalize launch advances by 1 once the
+        # noise has read it (args.mpvae_seed_advance), or None
+        self.seed_advance = seed_advance
         self.exchange = exchange if exchange is not None else LocalExchange()
 
 
@@ -323,21 +381,34 @@ class ProbitELBO(torch.autograd.Function):
         z = R.shape[1]
         cfg.exchange.verify_replicas((y, fe_out, fx_out, R))
         shape = be.shape(cfg.S_local, cfg.S_total, cfg.s_offset, B, L, z)
-        if cfg.noise == "philox":
-            eps = be.make_noise(shape, y.device, cfg.seed, cfg.offset)
+        if cfg.noise == "philox" and hasattr(be, "make_noise_and_R"):
+            # small r_sqrt_sigma: its split rides on the noise launch
+            eps, Rop = be.make_noise_and_R(shape, y.device, cfg.seed, cfg.offset, R)
         else:
-            eps = _f32(eps, "noise")
-            if tuple(eps.shape) != (cfg.S_local, B, z):
-                raise ValueError(f"noise must be {(cfg.S_local, B, z)}, got {tuple(eps.shape)}")
-            eps = be.prepare_noise(eps, shape)
-        Rop = be.prepare_R(R)
+            if cfg.noise == "philox":
+                eps = be.make_noise(shape, y.device, cfg.seed, cfg.offset)
+            else:
+                eps = _f32(eps, "noise")
+                if tuple(eps.shape) != (cfg.S_local, B, z):
+                    raise ValueError(f"noise must be {(cfg.S_local, B, z)}, "
+                                     f"got {tuple(eps.shape)}")
+                eps = be.prepare_noise(eps, shape)
+            Rop = be.prepare_R(R)
         need = ctx.needs_input_grad
         keep_T = need[1] or need[4] or need[7]
+        fin = (fe_mu, fe_logvar, fx_mu, fx_logvar, cfg.nll_coeff, cfg.c_coeff)
+        adv = {} if cfg.seed_advance is None else {"seed_advance": cfg.seed_advance}
         loc = be.forward_local(shape, y, fe_out, fx_out, Rop, eps, keep_T,
                                stat_slots=cfg.exchange.stat_slots())
-        bstat, colsum = cfg.exchange.combine(loc, be)
-        outs = be.finalize(shape, bstat, colsum, fe_mu, fe_logvar, fx_mu, fx_logvar,
-                           cfg.nll_coeff, cfg.c_coeff)
+        gathered = (cfg.exchange.gather_slots(loc)
+                    if hasattr(be, "finalize_slots") and hasattr(cfg.exchange, "gather_slots")
+                    else None)
+        if gathered is not None:
+            # sharded: the exact cross-shard combine inside the finalize launch
+            bstat, outs = be.finalize_slots(shape, gathered[0], gathered[1], *fin, **adv)
+        else:
+            bstat, colsum = cfg.exchange.combine(loc, be)
+            outs = be.finalize(shape, bstat, colsum, *fin, **adv)
         ctx.set_materialize_grads(False)
         ctx.cfg, ctx.shape, ctx.r_dtype, ctx.keep_T = cfg, shape, R.dtype, keep_T
         ctx.consumed = False
@@ -358,8 +429,15 @@ class ProbitELBO(torch.autograd.Function):
         gs = [g_total, g_nll, g_nll_x, g_c, g_c_x, g_kl]
         live = sum(1 << i for i, g in enumerate(gs) if g is not None)
         dev = sv["y"].device
-        zero = torch.zeros((), device=dev, dtype=torch.float32)
-        gscal = torch.stack([zero if g is None else g.reshape(()).to(torch.float32) for g in gs])
+        if getattr(be, "reads_live_slots", False) and live == 1:
+            # total_loss.backward() alone: the kernels read only the live slot,
+            # so the upstream gradient's own storage is gscal (no zeros + stack:
+            # two launches fewer per step)
+            gscal = gs[0].reshape((1,)).to(torch.float32).contiguous()
+        else:
+            zero = torch.zeros((), device=dev, dtype=torch.float32)
+            gscal = torch.stack([zero if g is None else g.reshape(()).to(torch.float32)
+                                 for g in gs])
         g_I = None if g_I is None else g_I.to(torch.float32).contiguous()
         g_IL = None if g_IL is None else g_IL.to(torch.float32).contiguous()
         grads = [None] * 10
@@ -387,7 +465,8 @@ class ProbitELBO(torch.autograd.Function):
         if want_kl:
             if gk is None:
                 gk = be.kl_backward(sv["fe_mu"], sv["fe_logvar"], sv["fx_mu"], sv["fx_logvar"],
-                                    gscal)
+                                    gscal, **({"live": live} if getattr(be, "reads_live_slots",
+                                                                       False) else {}))
             grads[2], grads[3], grads[5], grads[6] = gk
         ctx.saved = None
         return tuple(grads)

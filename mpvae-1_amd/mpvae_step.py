@@ -16,6 +16,7 @@ fairsoft_train.py:154-162).  Each sync drains the stream.  Here:
 Both are torch glue around the loop, not kernels of the hot path: they run on
 whatever device the tensors live on.
 """
+import copy
 import ctypes
 import functools
 
@@ -313,10 +314,15 @@ class TrainStep:
         import mpvae
         self.opt.zero_grad(set_to_none=True)
         seed = getattr(self.args, "mpvae_seed", None)
+        args = self.args
         if self.advance_seed and isinstance(seed, torch.Tensor):
-            seed.add_(1)  # fresh probit noise every step, on the device
+            # fresh probit noise every step, on the device: compute_loss's
+            # finalize launch advances the key after the noise has read it
+            # (args.mpvae_seed_advance; no launch of its own)
+            args = copy.copy(self.args)
+            args.mpvae_seed_advance = True
         out = self.model(label, feat)
-        res = mpvae.compute_loss(label, *out, self.model.r_sqrt_sigma, self.args)
+        res = mpvae.compute_loss(label, *out, self.model.r_sqrt_sigma, args)
         res[0].backward()
         self._clip()
         # finite gate: the AMP multi-tensor check (one launch per dtype) sets

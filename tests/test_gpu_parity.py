@@ -192,6 +192,58 @@ def test_graph_captured_step_draws_fresh_noise_per_replay():
             assert torch.equal(a, v.grad)
 
 
+@pytest.mark.parametrize("key_on_device", [True, False])
+@pytest.mark.parametrize("L,z,rdt", [(38, 38, torch.float64), (81, 81, torch.float32),
+                                     (128, 128, torch.float64), (3, 2, torch.float64)])
+def test_noise_with_r_split_is_the_two_launches(L, z, rdt, key_on_device):
+    """mpv_noise_philox_f16_split (the r_sqrt_sigma split riding on the noise
+    launch, L * z <= 16384) writes exactly what mpv_noise_philox_f16(_dev) and
+    mpv_split_f16 write: planes and scales bit for bit."""
+    be = HipShardBackend("f16x3")
+    shape = be.shape(37, 50, 13, 6, L, z)
+    g = torch.Generator(device=DEV).manual_seed(L + z)
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=rdt) * 2 - 1) * 0.3
+    key = torch.tensor([987654321], dtype=torch.int64, device=DEV) if key_on_device else 987654321
+    eps, Rop = be.make_noise_and_R(shape, DEV, key, 5, R)
+    eps2, Rop2 = be.make_noise(shape, DEV, key, 5), be.prepare_R(R)
+    assert torch.equal(Rop.scale, Rop2.scale) and torch.equal(Rop.data, Rop2.data)
+    # the noise planes as far as the noise kernel writes them (z up to the
+    # 32-wide K slice; the dR tile's padding beyond is left unwritten)
+    w = 2 * ((z + 31) // 32 * 32)
+    assert torch.equal(eps.scale, eps2.scale)
+    assert torch.equal(eps.data[:, :w], eps2.data[:, :w])
+
+
+def test_seed_advance_in_finalize():
+    """args.mpvae_seed_advance: the finalize launch advances the device key by
+    one after the step's noise has read it -- the outputs are those of the
+    key's value at the call, and the next call draws the next key's noise."""
+    B, L, z, d, S = 8, 12, 12, 4, 16
+    g = torch.Generator(device=DEV).manual_seed(21)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.3).float()
+    y[:, 0], y[:, 1] = 1, 0
+    base = [torch.randn((B, L), device=DEV, generator=g), torch.randn((B, d), device=DEV, generator=g),
+            torch.randn((B, d), device=DEV, generator=g), torch.randn((B, L), device=DEV, generator=g),
+            torch.randn((B, d), device=DEV, generator=g), torch.randn((B, d), device=DEV, generator=g),
+            torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) - 0.5]
+    mk = lambda sd, adv: argparse.Namespace(label_dim=L, z_dim=z, n_train_sample=S,
+                                            n_test_sample=S, mode="train", nll_coeff=0.5,
+                                            c_coeff=10.0, mpvae_noise="philox", mpvae_seed=sd,
+                                            mpvae_seed_advance=adv)
+    seed = torch.tensor([777], dtype=torch.int64, device=DEV)
+    a1 = mpvae.compute_loss(y, *base, mk(seed, True))
+    assert int(seed) == 778
+    a2 = mpvae.compute_loss(y, *base, mk(seed, True))
+    assert int(seed) == 779
+    r1 = mpvae.compute_loss(y, *base, mk(777, False))
+    r2 = mpvae.compute_loss(y, *base, mk(778, False))
+    for a, r in ((a1, r1), (a2, r2)):
+        for u, v in zip(a, r):
+            assert torch.equal(u, v)
+    with pytest.raises(ValueError, match="seed_advance"):
+        mpvae.compute_loss(y, *base, mk(777, True))
+
+
 def test_split_planes_round_trip():
     """mpv_split_f16: power-of-two scale from max|x|, hi+lo == x to ~2^-22."""
     be = HipShardBackend("f16x3")
