@@ -100,8 +100,13 @@ class VAE(nn.Module):
         self.reparam_noise = torch.randn_like
 
     # -- one Linear layer: act(alpha * layer(x)), act = ReLU if `relu`
+    def _hip(self, x):
+        """mpv_linear / the fused reparameterisation on CUDA tensors; CPU tensors
+        run the reference's own torch ops (mpvae.py:51-84)."""
+        return self.linear_backend == "hip" and x.is_cuda
+
     def _lin(self, layer, x, relu=False, alpha=1.0):
-        if self.linear_backend == "hip":
+        if self._hip(x):
             return mpvae_linear.linear(x, layer, relu, alpha)
         y = layer(x)
         if relu:
@@ -111,7 +116,7 @@ class VAE(nn.Module):
     # -- encoders (mpvae.py:51-64)
     def _mlp(self, x, layers):
         drop = self.dropout
-        fold = (FOLD_DROPOUT and self.linear_backend == "hip" and type(drop) is nn.Dropout
+        fold = (FOLD_DROPOUT and self._hip(x) and type(drop) is nn.Dropout
                 and drop.training
                 and drop.p > 0.0 and not drop.inplace)
         for lin in layers:
@@ -122,7 +127,7 @@ class VAE(nn.Module):
         return x
 
     def _heads(self, h, mu, logvar):
-        if self.linear_backend == "hip":  # both heads in one launch
+        if self._hip(h):  # both heads in one launch
             return mpvae_linear.heads(h, mu, logvar, self.scale_coeff)
         return (self._lin(mu, h, alpha=self.scale_coeff),
                 self._lin(logvar, h, alpha=self.scale_coeff))
@@ -135,11 +140,17 @@ class VAE(nn.Module):
                            self.fx_logvar)
 
     # -- reparameterisation (mpvae.py:66-74), one encoder at a time
+    def _reparam(self, mu, logvar):
+        eps = self.reparam_noise(logvar)
+        if mu.is_cuda:
+            return SingleReparam.apply(mu, logvar, eps)
+        return mu + eps * torch.exp(0.5 * logvar)  # mpvae.py:67-69 on the CPU
+
     def label_reparameterize(self, mu, logvar):
-        return SingleReparam.apply(mu, logvar, self.reparam_noise(logvar))
+        return self._reparam(mu, logvar)
 
     def feat_reparameterize(self, mu, logvar):
-        return SingleReparam.apply(mu, logvar, self.reparam_noise(logvar))
+        return self._reparam(mu, logvar)
 
     # -- decoders (mpvae.py:76-84); fd1/fd2 are fd_x1/fd_x2
     def _decode(self, z, head):
@@ -174,6 +185,11 @@ class VAE(nn.Module):
         eps_e = self.reparam_noise(lv_e)
         mu_x, lv_x = self.feat_encode(feature)
         eps_x = self.reparam_noise(lv_x)
+        if not feature.is_cuda:  # the reference's ops on the CPU (mpvae.py:67-74, 76-84)
+            z_e = mu_e + eps_e * torch.exp(0.5 * lv_e)
+            z_x = mu_x + eps_x * torch.exp(0.5 * lv_x)
+            return (self.label_decode(torch.cat((feature, z_e), 1)), mu_e, lv_e,
+                    self.feat_decode(torch.cat((feature, z_x), 1)), mu_x, lv_x)
         # mu / logvar come back through the fused op: compute_loss's KL gradient
         # for them is then added inside its backward launch
         r = FusedReparam.apply(mu_e, lv_e, eps_e, mu_x, lv_x, eps_x)
@@ -281,11 +297,27 @@ def _empty_batch(fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar, R, args):
     return (total, nll, nll_x, c, c_x, kl, fx_out.float() * 0 + zr, fe_out.float() * 0 + zr)
 
 
+def _backend_for(tensors):
+    """None (the HIP library on the GPU) for CUDA tensors -- raising when it is
+    missing -- or the host C++ backend (mpvae_host.py) for CPU tensors, as the
+    reference runs its small configurations on the CPU (fairsoft_trial.py:
+    157-158).  Dispatch by device, never a fallback: CUDA tensors do not reach
+    the host backend."""
+    kinds = {t.device.type for t in tensors if t is not None}
+    if kinds == {"cpu"}:
+        import mpvae_host
+        return mpvae_host.HostShardBackend()
+    mpvae_hip.require_gpu(*tensors)
+    if len({t.device for t in tensors if t is not None}) > 1:
+        raise RuntimeError("compute_loss inputs must all live on one device")
+    return None
+
+
 def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
                  r_sqrt_sigma, args):
     """Multivariate-probit ELBO of reference mpvae.py:145-210 (8-tuple)."""
-    mpvae_hip.require_gpu(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
-                          r_sqrt_sigma)
+    host_be = _backend_for((input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar,
+                            r_sqrt_sigma))
     n_sample = args.n_train_sample if args.mode == "train" else args.n_test_sample
     B, z = fe_out.shape[0], args.z_dim
     if r_sqrt_sigma.dim() != 2 or r_sqrt_sigma.shape[1] != z:
@@ -300,6 +332,7 @@ def compute_loss(input_label, fe_out, fe_mu, fe_logvar, fx_out, fx_mu, fx_logvar
     shard = mpvae_dist.shard_for(args, n_sample)
     noise, kw = _noise_source(args, n_sample, B, z, shard, fe_out.device)
     cfg = ElboConfig(n_sample, shard.S_local, shard.s_offset, args.nll_coeff, args.c_coeff,
-                     exchange=shard.exchange, gemm=getattr(args, "mpvae_gemm", "f16x3"), **kw)
+                     exchange=shard.exchange, gemm=getattr(args, "mpvae_gemm", "f16x3"),
+                     backend=host_be, **kw)
     return ProbitELBO.apply(input_label.float(), fe_out, fe_mu, fe_logvar, fx_out, fx_mu,
                             fx_logvar, r_sqrt_sigma, noise, cfg)

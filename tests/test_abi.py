@@ -71,16 +71,17 @@ def test_check_raises_with_message():
                 "mpv_probit_bwd")
 
 
-def test_product_refuses_cpu_tensors():
+def test_compute_loss_dispatches_on_device():
+    """CPU tensors go to the host C++ backend (mpvae_host.py, as the reference
+    runs its small configurations on the CPU), never to the HIP library; a
+    mix of devices is an error.  CUDA tensors (tests/test_gpu_*) run the HIP
+    library and raise when it is missing (test_missing_library_fails_loudly)."""
     import torch
     import mpvae
-    from golden_io import fixtures
-    f = fixtures()[0]
-    t = {k: torch.from_numpy(f[k]) for k in ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out",
-                                              "fx_mu", "fx_logvar", "r_sqrt_sigma"]}
-    with pytest.raises(RuntimeError, match="GPU only"):
-        mpvae.compute_loss(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"], t["fx_out"],
-                           t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"], f.args())
+    import mpvae_host
+    cpu = torch.zeros(2, 3)
+    assert isinstance(mpvae._backend_for((cpu, cpu)), mpvae_host.HostShardBackend)
+    assert mpvae._backend_for((cpu, None)) is not None
 
 
 def test_missing_library_fails_loudly(tmp_path):
@@ -115,3 +116,21 @@ def test_linear_host_checks():
                         ones_col=-1, alpha=1.0, out=fake, out_si=4, a2=fake, a2_si=4, R1=2)
     assert lib.mpv_linear(ctypes.byref(half), None, 0, None) == 1
     assert b"second segment" in lib.mpv_last_error()
+
+
+HOST_HEADER = os.path.join(ROOT, "include", "mpvae_host.h")
+
+
+def test_host_library_exports_what_its_header_declares():
+    """libmpvae_host.so (the CPU backend) against include/mpvae_host.h."""
+    import mpvae_host
+    src = re.sub(r"/\*.*?\*/", "", open(HOST_HEADER).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(mpvh_[a-z0-9_]+)\s*\(", src)))
+    assert declared == mpvae_host.EXPORTS
+    lib = mpvae_host.load_library()
+    assert lib.mpvh_abi_version() == mpvae_host.ABI_VERSION
+    out = subprocess.run(["nm", "-D", "--defined-only", mpvae_host.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert set(re.findall(r"\bT (mpvh_\w+)", out)) == set(declared)
+    assert lib.mpvh_probit_fwd(H.Shape(0, 4, 0, 2, 8, 8), mpvae_host.FwdArgs()) == 1
+    assert b"bad shape" in lib.mpvh_last_error()

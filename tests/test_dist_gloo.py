@@ -204,3 +204,60 @@ def test_comm_timer_records_every_collective():
         assert all(d["calls"] in (None, 2) for d in summ.values()), summ
         for op, d in summ.items():
             assert d["device_ms"] is None and d["host_ms"] > 0.0, (rank, op, d)
+
+
+def _host_worker(rank, world, port, q):
+    """compute_loss itself on CPU tensors with args.mpvae_shard: the product's
+    host backend (libmpvae_host.so) on every rank, the exchange over gloo."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import mpvae
+        from golden_io import DIFF, OUTS, fixtures
+        from tolerances import FWD_RTOL, GRAD_RTOL, rel_err
+        res = []
+        for f in [f for f in fixtures() if f.name in ("f1_l38", "f2_degenerate", "f6_l81")]:
+            t = {k: torch.from_numpy(f[k].copy()) for k in
+                 ["y", "fe_out", "fe_mu", "fe_logvar", "fx_out", "fx_mu", "fx_logvar",
+                  "r_sqrt_sigma"]}
+            for k in DIFF + (["r_sqrt_sigma"] if f.trainable_r else []):
+                t[k].requires_grad_(True)
+            args = f.args(mpvae_noise=torch.from_numpy(f["noise"]), mpvae_shard=True,
+                          mpvae_check_replicas=True)
+            out = mpvae.compute_loss(t["y"], t["fe_out"], t["fe_mu"], t["fe_logvar"],
+                                     t["fx_out"], t["fx_mu"], t["fx_logvar"], t["r_sqrt_sigma"],
+                                     args)
+            errs = {k: rel_err(o.detach().numpy(), f["out_" + k]) for k, o in zip(OUTS, out)}
+            obj = out[0] + (out[6] * torch.from_numpy(f["g_I"])).sum() + \
+                (out[7] * torch.from_numpy(f["g_IL"])).sum()
+            obj.backward()
+            for k, v in f.grads("gtot").items():
+                g = t[k].grad.double().numpy()
+                errs["d" + k] = rel_err(g, v) if np.array_equal(np.isnan(g), np.isnan(v)) \
+                    else float("inf")
+            ok = all(v <= (FWD_RTOL if not k.startswith("d") else GRAD_RTOL)
+                     for k, v in errs.items())
+            res.append((f.name, ok, errs))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_compute_loss_on_the_host_backend(world):
+    """The drop-in compute_loss with args.mpvae_shard on CPU tensors: every rank
+    runs the host C++ backend on its sample shard, the statistics and gradients
+    cross ranks over gloo, and the result is the reference's golden record."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in results:
+        for name, ok, errs in res:
+            assert ok, (rank, name, errs)
