@@ -766,7 +766,7 @@ MPV_DEV void dr_read(DrFrag<TM, TN>& f, const char* base, int wm, int wn, int r0
 // dr_read with a group-0 wave's share of the next stage's LDS-DMA woven in:
 // one or two 1-KB pieces after each tile's four transposed reads, so the
 // CU's load path (the DMA) and the LDS (the reads) work side by side instead
-// of the reads queueing behind the whole DMA burst (tools/dr_stamps.py: DMA
+// of the reads queueing behind the whole DMA burst (tools/studies/dr_stamps.py: DMA
 // issue 1060 + reads 960 ticks, serial, against 1650 for the other group's
 // MFMAs).  Noise rows past the last real one (a padded last stage) repeat
 // that row, as drs_issue_range clamps them.
@@ -847,7 +847,7 @@ MPV_DEV void drs_issue_range(const Dr16Params& p, char* dst, int q0, int rows, i
   }
 }
 
-// Timing study (MPV_DR_STAMPS=1 builds only, tools/dr_stamps.py): s_memtime
+// Timing study (MPV_DR_STAMPS=1 builds only, tools/studies/dr_stamps.py): s_memtime
 // at the slot boundaries of workgroup 0's waves over its first kDrStampStages
 // stages, stored by lane 0 with vector stores; read back through
 // mpv_study_dr_stamps.
@@ -910,7 +910,7 @@ struct DrsDma {
 //   mma(i): 96 MFMAs; group 0 then waits for its stage i+1 DMA, so stage i+1
 //           is visible to both groups after the slot's barrier.
 // Two 64-KB stage images; DMA latency budget = one slot pair.  Round 5
-// (tools/dr_stamps.py, profiles/r05_dr_ab.json): with the DMA as a burst ahead
+// (tools/studies/dr_stamps.py, profiles/r05_dr_ab.json): with the DMA as a burst ahead
 // of the reads, group 0's mem slot (1060 + 960 ticks) outlasted the other
 // group's MFMAs (1650) every slot; woven, dR -4.2 %.  Measured slower: group 1
 // issuing the stream between its own MFMAs (+2.3 %), half of it in each

@@ -918,7 +918,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // label-branch update of one 16-lane row with the pad in place, with no
   // inline asm at all, with ds_bpermute sums instead of permlanes, and without
   // the T stash; only one workgroup per CU removes it.  DESIGN.md section 3,
-  // "the round-3 lost update", tools/race_study.sh.)
+  // "the round-3 lost update", tools/studies/race_study.sh.)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 1" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);

@@ -147,7 +147,7 @@ def test_vae_linear_backends_agree():
     nn.Linear run's ReLU masks forced to the hip run's.  (Without the forcing a
     pre-activation within rounding of 0 -- 1.5e-8 in this case -- flips its
     ReLU between any two fp32 GEMMs and moves the decoder's weight gradient
-    by 3.4e-3: tools/vae_linear_probe.py.)"""
+    by 3.4e-3: tools/studies/vae_linear_probe.py.)"""
     import argparse
 
     import mpvae

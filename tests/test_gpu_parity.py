@@ -681,7 +681,7 @@ def test_c5_full_size_against_fp64_reference(seed):
     arithmetic on the kernels' own t are measured against the fp64 one too,
     as at C4 (_assert_c45).  Seed 11 is the case where the f16x3 kernels land
     3.6e-3 from fp64-t: one sample one fp32 ulp of E from 1
-    (tools/c5_worst.py, profiles/r05_c5_seed11_worst.json)."""
+    (tools/studies/c5_worst.py, profiles/r05_c5_seed11_worst.json)."""
     from torch64_ref import ChunkedElbo
     (B, S, L, z, d, _), y, fe, fx, mus, R = _prop_inputs("c5", seed)
     key = 55490 + seed

@@ -48,7 +48,7 @@ HEADLINE_GRAD_RTOL = 5e-4
 # fp32 ulp below 1 (1 - E ~ 1e-6, one ulp ~ 6 % of it): any fp32 computation
 # of t that rounds differently moves such an element's gradient by ~0.3 %, and
 # the normwise error of the whole tensor with it.  Measured over 5 seeds
-# (tools/c4_spread.py, profiles/r04_c4_spread.json): the reference's own fp32
+# (tools/studies/c4_spread.py, profiles/r04_c4_spread.json): the reference's own fp32
 # arithmetic (t from an fp32 GEMM, as its tensordot) lands <= 5.6e-4 from the
 # fp64-t values, the kernels <= 6.8e-4 (f16x3) and <= 5.6e-4 (exact-fp32
 # MFMA mode), each worst case a different single element; on the B = 512,
@@ -69,7 +69,7 @@ C4_FULL_GRAD_RTOL = 1.5e-3
 # fp32 erf <= 1.5e-3, the f16x3 kernels <= 1.6e-3 on three seeds and 3.6e-3
 # on one (seed 11, d fe_out; there the exact-fp32 MFMA mode gives 1.06e-3 and
 # the fp32 reference 1.04e-3: a different set of one-ulp roundings, not a
-# bias -- tools/t_accuracy.py finds the 3xf16 t closer to the fp64 product
+# bias -- tools/studies/t_accuracy.py finds the 3xf16 t closer to the fp64 product
 # than an fp32 GEMM's, mean |err| 5.0e-7 against 8.0e-7 at K = 4096).  The
 # tests assert the reference's own spread under the same bound, and the
 # per-case rule of C4 (_assert_c45).

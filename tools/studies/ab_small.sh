@@ -1,4 +1,4 @@
-# A/B of dR variants at the small configs (tools/ablate.sh build first)
+# A/B of dR variants at the small configs (tools/studies/ablate.sh build first)
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out/ab

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Build forward-kernel variants into abl/<name>/libmpvae_hip.so:
-#   tools/abl_fwd.sh name "-DFLAG=1 -DOTHER=2" [name "flags"] ...
+#   tools/studies/abl_fwd.sh name "-DFLAG=1 -DOTHER=2" [name "flags"] ...
 set -e
-R="$(cd "$(dirname "$0")/.." && pwd)"
+R="$(cd "$(dirname "$0")/../.." && pwd)"
 cd "$R/mpvae-1_amd" && make -s >/dev/null
 while [ $# -gt 1 ]; do
   n=$1; f=$2; shift 2

@@ -3,9 +3,9 @@
 # abl/<variant>/ (here: `build`) and times them on the GPU box (`run`).
 # A variant is <bits>[:<extra>...]: <bits> = MPV_ABL (probit_fwd.hip /
 # probit_bwd.hip / util.hip); each ':'-separated extra is MACRO=value (-D) or a raw -flag.
-# The MPV_ABL hooks are not in the product sources: tools/ablation_hooks.patch
+# The MPV_ABL hooks are not in the product sources: tools/studies/ablation_hooks.patch
 # adds them to a copy of csrc/ per variant (with MPV_ABL=0 the product's ISA).
-R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 VARIANTS="${VARIANTS:-0 1 5 9 17 13 25}"
 dir_of() { echo "$R/abl/$(echo "$1" | tr ':=' '__' | tr -d ' ')"; }
 case "$1" in
@@ -13,7 +13,7 @@ case "$1" in
     cd "$R/mpvae-1_amd" && make -s >/dev/null || exit 1
     for v in $VARIANTS; do
       d=$(dir_of "$v"); mkdir -p "$d"
-      rm -rf "$d/csrc" && cp -r csrc "$d/csrc" && patch -s -p1 -d "$d/csrc" < "$R/tools/ablation_hooks.patch" || exit 1
+      rm -rf "$d/csrc" && cp -r csrc "$d/csrc" && patch -s -p1 -d "$d/csrc" < "$R/tools/studies/ablation_hooks.patch" || exit 1
       bits=${v%%:*}; extra=""
       if [[ "$v" == *:* ]]; then   # extras: MACRO=value or a raw -flag, ':'-separated
         IFS=':' read -ra parts <<< "${v#*:}"

@@ -4,7 +4,7 @@ weights + fwd + bwd) and the train metrics, against the CPU oracle of the same
 computation (oracle/fairness.py: the reference's loop structure -- a Python
 dict lookup per row, group masks -- in numpy, single thread).
 
-    python tools/bench_consumers.py [--reps 20]
+    python tools/studies/bench_consumers.py [--reps 20]
 Prints one JSON line.
 """
 import argparse
@@ -15,7 +15,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402

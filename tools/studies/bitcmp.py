@@ -1,8 +1,8 @@
 """Bit-for-bit comparison of two library builds' backward outputs.
 
-  MPVAE_HIP_LIB=<lib A> python tools/bitcmp.py dump A.pt
-  MPVAE_HIP_LIB=<lib B> python tools/bitcmp.py dump B.pt
-  python tools/bitcmp.py cmp A.pt B.pt
+  MPVAE_HIP_LIB=<lib A> python tools/studies/bitcmp.py dump A.pt
+  MPVAE_HIP_LIB=<lib B> python tools/studies/bitcmp.py dump B.pt
+  python tools/studies/bitcmp.py cmp A.pt B.pt
 
 Cases: binary labels at L = 1024 (every wave full), L = 1100 (masked
 columns), soft labels, and a degenerate row (all labels 1: NaN row
@@ -12,7 +12,7 @@ must print "identical" for all of them."""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402
 

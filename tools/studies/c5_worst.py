@@ -13,8 +13,8 @@ Decomposes the kernels' error against the fp64-t restatement
 and records the worst elements of d fe_out / d fx_out with the sample terms
 that dominate them (t under each arithmetic, E and 1 - E in fp32).
 
-  python tools/c5_worst.py --seed 11 [--config c5|c4] > out.json
-  python tools/c5_worst.py --c4test 3 > out.json   (the inputs of
+  python tools/studies/c5_worst.py --seed 11 [--config c5|c4] > out.json
+  python tools/studies/c5_worst.py --c4test 3 > out.json   (the inputs of
       tests/test_gpu_parity.py::test_c4_full_size_against_fp64_reference, explicit
       noise; adds the forward row statistics of the worst rows: the kernels'
       rowstat against the reference's formulas on the kernels' own t)
@@ -24,7 +24,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "mpvae-1_amd"), os.path.join(ROOT, "tests")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

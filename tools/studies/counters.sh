@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ/TCC counter passes (one rocprofv3 --pmc run per set) on the bench workload.
-# Usage on the GPU box: SETS="A B" bash tools/counters.sh ; results in gpurun_out/ctr/
-R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+# Usage on the GPU box: SETS="A B" bash tools/studies/counters.sh ; results in gpurun_out/ctr/
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 OUT="${CTR_OUT:-$R/gpurun_out/ctr}"
 ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline}"
 KRE="${KRE:-probit_fwd|dR16|dR_gemm|bwd_elem|noise}"

@@ -2,12 +2,12 @@
 buffers differ (bitwise), and where: noise planes, forward rowstat / bstat /
 colsum / T, finalize outputs, backward buffers.
 
-    python tools/determinism_probe.py B S L z [reps]
+    python tools/studies/determinism_probe.py B S L z [reps]
 """
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@ build of the library (MPV_DR_STAMPS=1):
 
   cd mpvae-1_amd && hipcc ... -DMPV_DR_STAMPS=1 -c csrc/probit_bwd.hip -o ../scratch/drS/probit_bwd.o
   (link with the other objects into scratch/drS/libmpvae_hip.so)
-  MPVAE_HIP_LIB=scratch/drS/libmpvae_hip.so python tools/dr_stamps.py [B S L z] > out.json
+  MPVAE_HIP_LIB=scratch/drS/libmpvae_hip.so python tools/studies/dr_stamps.py [B S L z] > out.json
 
 Stamp points per stage i (dR16s_kernel, DR_G0_STAGE / DR_G1_STAGE):
   0 slot start, 1 group 0 after its LDS-DMA issue, 2 after the fragment reads
@@ -19,7 +19,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -1,5 +1,5 @@
 """Host-side (Python) cost of one eager compute_loss forward + backward:
-cProfile of N calls at a small config.  python tools/eager_profile.py [c2|c3]"""
+cProfile of N calls at a small config.  python tools/studies/eager_profile.py [c2|c3]"""
 import argparse
 import cProfile
 import os
@@ -7,7 +7,7 @@ import pstats
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402
 

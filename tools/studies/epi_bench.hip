@@ -8,8 +8,8 @@
 // variants that drop one class of instruction at a time.  Prints cycles per
 // block per SIMD (s_memtime of the slowest wave) for 1 and 2 waves per SIMD.
 //
-//   hipcc --offload-arch=gfx950 -O3 -I../mpvae-1_amd/csrc -I../include \
-//         tools/epi_bench.hip -o scratch/epi_bench && scratch/epi_bench
+//   hipcc --offload-arch=gfx950 -O3 -I../../mpvae-1_amd/csrc -I../../include \
+//         tools/studies/epi_bench.hip -o scratch/epi_bench && scratch/epi_bench
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box pass: parity tests, smoke, bench.  Stops at the first step that
 # ends in a signal / timeout (GPU fault, abort, hang); test failures (rc 1) go on.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 ok_or_fail() {  # rc, step
   local rc=$1

@@ -16,7 +16,7 @@ Only reports a pair when the producer or the consumer sits inside an
 between the two ends the window (control may arrive from elsewhere; those
 paths are reported separately with the label noted).
 
-    python tools/hazard_scan.py file.s [kernel-substring]
+    python tools/studies/hazard_scan.py file.s [kernel-substring]
 """
 import re
 import sys

@@ -3,7 +3,7 @@ the eager step is host-bound (C2: ~0.3 ms eager against 0.13 ms as a HIP
 graph): cProfile over N steps of bench.step, the device synchronised only at
 the end, top functions by own time.
 
-  python tools/host_profile.py [--config c2] [--steps 200]
+  python tools/studies/host_profile.py [--config c2] [--steps 200]
 """
 import argparse
 import cProfile
@@ -13,7 +13,7 @@ import pstats
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mpvae-1_amd")]
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@ register the inline asm names, compiler AGPR moves, scratch, and M0 writes outsi
 inline asm.
 
   hipcc --offload-arch=gfx950 -O3 ... --cuda-device-only -S probit_fwd.hip -o fwd.s
-  python tools/isa_audit.py fwd.s <mangled kernel name>
+  python tools/studies/isa_audit.py fwd.s <mangled kernel name>
 """
 import re, sys, collections
 s=open(sys.argv[1]).read()

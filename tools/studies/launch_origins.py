@@ -3,7 +3,7 @@
 the launch count per step and the innermost aten ops / Python frames that
 issued it.  A study tool for the drop-in training step.
 
-    python tools/launch_origins.py [--config c2] [--kernel direct_copy]
+    python tools/studies/launch_origins.py [--config c2] [--kernel direct_copy]
 """
 import argparse
 import collections

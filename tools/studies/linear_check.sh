@@ -1,7 +1,7 @@
 #!/bin/bash
 # mpv_linear on one GPU box: its parity tests (errors recorded), the VAE / step
 # tests, the train step at C1-C3 (hip) and one aten-op listing.
-R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 O="$R/gpurun_out/${OUT:-lin}"
 mkdir -p "$O"
 cd "$R"

@@ -6,14 +6,14 @@ phase alone, the noise kernel alone, both serialised on one stream, and both
 issued on two streams (the noise on a side stream), with HIP events around
 the pair; writes gpurun_out/overlap_probe.json.
 
-    python tools/overlap_probe.py [reps]
+    python tools/studies/overlap_probe.py [reps]
 """
 import json
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402
 

@@ -3,7 +3,7 @@
 torch.profiler over a few steps of bench.py's step function, device kernels,
 memsets and memcpys grouped by the top-level op that issued them.
 
-  python tools/step_ops.py [--n-sample 512]
+  python tools/studies/step_ops.py [--n-sample 512]
 
 (The sharded path on a world-of-one RCCL group is profiled with a rocprofv3
 kernel trace of MPVAE_FORCE_DIST=1 bench.py instead: under torch.profiler that
@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mpvae-1_amd")]
 import torch  # noqa: E402
 

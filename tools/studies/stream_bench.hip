@@ -10,7 +10,7 @@
 //   elem4x2 : as elem4 with two rows per iteration (more loads in flight)
 // each with default and nontemporal policy.  Prints TB/s of (read + write).
 //
-//   hipcc --offload-arch=gfx950 -O3 tools/stream_bench.hip -o scratch/stream_bench
+//   hipcc --offload-arch=gfx950 -O3 tools/studies/stream_bench.hip -o scratch/stream_bench
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -5,13 +5,13 @@ at a C4/C5-like K.  Reports, per mode, max and rms |t - t64| in units of
 ulp(t64) and the mean signed error (a bias would add up over the labels of the
 per-sample log-likelihood).  Writes gpurun_out/t_accuracy.json.
 
-    python tools/t_accuracy.py [z] [B] [S]
+    python tools/studies/t_accuracy.py [z] [B] [S]
 """
 import json
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 import torch  # noqa: E402
 

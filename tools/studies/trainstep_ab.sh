@@ -4,7 +4,7 @@
 # tools/trainstep_profile.py ("b", default --no-passthrough).  Stops at the
 # first failing step.
 set -o pipefail
-R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 O="$R/gpurun_out/${OUT:-trainstep_ab}"
 mkdir -p "$O"
 cd "$R"

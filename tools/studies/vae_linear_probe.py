@@ -1,14 +1,14 @@
 """Where do the VAE's gradients with mpv_linear and with nn.Linear part?
 Per Linear call: the kernel's own error against fp64 on the SAME inputs
 (x, upstream gradient, ReLU mask), and how far the two backends' inputs to
-that call already differ.  python tools/vae_linear_probe.py [B]"""
+that call already differ.  python tools/studies/vae_linear_probe.py [B]"""
 import argparse
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "mpvae-1_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
