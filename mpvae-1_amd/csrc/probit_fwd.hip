@@ -1398,8 +1398,8 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
-  // 3xf16: s-chunks until the grid is one round of resident workgroups (2
-  // per CU for the 48-label tile, 1 for the 8-wave tiles); longer runs per
+  // 3xf16: s-chunks until the grid is one round of resident workgroups (one
+  // per CU: every 3xf16 tile is 8 waves); longer runs per
   // workgroup amortize its prologue (C3 step 0.534 -> 0.510 ms against a
   // 2048-workgroup target, C2 the same; C4 has one s-chunk either way)
   const int64_t target = f16 ? (int64_t)num_cus() : kFwdWant;
