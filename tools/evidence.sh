@@ -9,6 +9,7 @@
 #   PART=bench    bench lines: C4 (headline), eval, C2 / C3 eager and graph
 #                 (C2 / C3 with the VALU roofline), C5 on one GPU, then the
 #                 rocprof trace + PMC passes of the headline (tools/profile.sh)
+#   PART=profsmall  rocprof trace + FETCH / WRITE / VALU passes at C2 and C3
 #   PART=scaling  one rank's share of the strong-scaling C4 step at 8 GPUs on
 #                 one GPU: n_sample 4096 vs 512, plain and through the sharded
 #                 path on a world-of-one RCCL group (MPVAE_FORCE_DIST=1)
@@ -57,6 +58,14 @@ bench)
   b c5_1gpu_bench --config c5 --no-cpu-baseline
   TAG=${TAG:-c4} bash tools/profile.sh || exit 1
   ;;
+profsmall)
+  # C2 / C3: trace + HBM + VALU passes (the VALU roofline and frac_algorithmic
+  # of bench.py read these once committed as profiles/<round>_c{2,3}_pmc.json)
+  for c in ${PROF_CONFIGS:-c2 c3}; do
+    TAG=$c BENCH_ARGS="--config $c --steps 50 --warmup 5 --no-cpu-baseline" \
+      STEPS="trace fetch write valu" bash tools/profile.sh || exit 1
+  done
+  ;;
 scaling)
   for S in 4096 512; do
     b s$S --n-sample $S --no-cpu-baseline
@@ -88,6 +97,6 @@ trainstep)
   done
   ;;
 *)
-  echo "PART must be tests, bench, scaling, gloo2 or trainstep"; exit 2 ;;
+  echo "PART must be tests, bench, profsmall, scaling, gloo2 or trainstep"; exit 2 ;;
 esac
 echo done
