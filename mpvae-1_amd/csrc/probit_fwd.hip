@@ -21,6 +21,9 @@
 // b), so fe/fx/y of the epilogue are per-lane constants and the column sums
 // over s stay in registers until the workgroup ends.  Workgroups sharing eps
 // rows (same b and s-chunk, other label tiles) get ids equal mod 8: one XCD.
+#include <cstdlib>
+#include <cstring>
+
 #include "abi_util.h"
 #include "mpv_common.h"
 
@@ -58,6 +61,30 @@ constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between schedu
 // 128: 26.8; round 5's MFMA-layout 48 x 128 tile, two workgroups per CU
 // without packed fp32: 33.4; same box, eager)
 constexpr int kFwd48BM = 256;
+#ifndef MPV_FWD_B
+#define MPV_FWD_B 1
+#endif
+#ifndef MPV_FWD_BA
+#define MPV_FWD_BA 10
+#endif
+constexpr bool kFwdB = MPV_FWD_B;  // L > 128: the 256 x 256 tile (probit_fwd16b)
+constexpr int kFwdBA = MPV_FWD_BA;  // its sample blocks on waves 0-3 (of 16)
+#ifndef MPV_FWD_BEPI
+#define MPV_FWD_BEPI 2
+#endif
+#ifndef MPV_FWD_BUNROLL
+#define MPV_FWD_BUNROLL 0
+#endif
+constexpr int kFwdBEpi = MPV_FWD_BEPI;
+#ifndef MPV_FWD_BPART
+#define MPV_FWD_BPART 2
+#endif
+constexpr int kFwdBPart = MPV_FWD_BPART;  // sample blocks per epilogue part of the 16b tile
+#ifndef MPV_FWD_BCQ
+#define MPV_FWD_BCQ 4
+#endif
+constexpr int kFwdBCQ = MPV_FWD_BCQ;  // column-sum slots per 16-lane row (1: lane 15, 4: quads)
+constexpr bool kFwdBUnroll = MPV_FWD_BUNROLL;
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
 constexpr int kLDK = 40;  // fp32 mode: LDS row stride in floats (conflict-free ds_read_b128)
@@ -737,7 +764,8 @@ MPV_DEV void pk_fma2_acc_bc(f32x2 p, f32x2 q, f32x2 r, f32x2& sp, f32x2& sn) {
 // 16 per-label masks of a label group would otherwise pin ~40 SGPRs and spill.
 // Every element is finite (R pad rows are zero, eps rows are clamped), so
 // weighting instead of selecting is exact.
-template <int WL, int WS, int TL, int TS, int BMT = WS * TS * 16>
+template <int WL, int WS, int TL, int TS, int BMT = WS * TS * 16, bool RED_IN_RING = false,
+          int EPI_BLOCKS = kEpiSampleBlocks, bool UNROLL_L = false, bool PUBLISH = true, int CQ = 1>
 MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float scale,
                                  int b, int s0, int s_own, int nt, float* red, float* cacc,
                                  const float* cols, bool soft_any, int sbo = -1) {
@@ -761,7 +789,8 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
   // unrolls fully without spilling, and the forward measures the same: C4
   // 13.28 / 13.25 vs 13.33 / 13.20 ms, so the rotation's moves are not on the
   // critical path)
-#pragma unroll 1
+  constexpr int kUnrollL = UNROLL_L ? TL : 1;
+#pragma unroll kUnrollL
   for (int m = 0; m < TL; ++m) {
     f32x4 am[TS];
 #pragma unroll
@@ -888,7 +917,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
         ce[i] = pk_fma(splat2(wr), E4[i], ce[i]);  // column sums of E over the wave's samples
       }
       // kEpiSampleBlocks samples at a time: bounded live ranges vs more independent chains
-      if ((n + 1) % kEpiSampleBlocks == 0) __builtin_amdgcn_sched_barrier(0);
+      if ((n + 1) % EPI_BLOCKS == 0) __builtin_amdgcn_sched_barrier(0);
     }
     // column sums of these 4 labels over the wave's samples: 16-lane trees
     // (8 chains step-major), lane 15 of each row accumulates into the
@@ -899,13 +928,31 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
       cs[2 * i] = ce[i].x;
       cs[2 * i + 1] = ce[i].y;
     }
-    row16_sum_to_lane15_n<8>(cs);
-    if (lr == 15) {
+    if (CQ == 4) {
+      // two DPP steps: the last lane of each quad holds the quad's sum, and
+      // the four quads of a row accumulate into their own slots (summed
+      // once per workgroup by fwd16t_colpart)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float* c = cacc + (ws * BN + lb + i) * 2;
-        c[0] += cs[2 * i];
-        c[1] += cs[2 * i + 1];
+      for (int j = 0; j < 8; ++j) cs[j] = dpp_f<0x111>(cs[j]) + cs[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] = dpp_f<0x112>(cs[j]) + cs[j];
+      if ((lr & 3) == 3) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float* c = cacc + ((ws * 4 + (lr >> 2)) * BN + lb + i) * 2;
+          c[0] += cs[2 * i];
+          c[1] += cs[2 * i + 1];
+        }
+      }
+    } else {
+      row16_sum_to_lane15_n<8>(cs);
+      if (lr == 15) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float* c = cacc + (ws * BN + lb + i) * 2;
+          c[0] += cs[2 * i];
+          c[1] += cs[2 * i + 1];
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // bound live ranges to one label group
@@ -935,12 +982,16 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
     v[n * 6 + 5] = sn[n].y;
   }
   sum_lanegroups_n<TS * 6>(v);  // all chains step-major
+  // red aliases the stage image the last K stage was read from: every wave
+  // is past its fragment reads once all have met here
+  if (RED_IN_RING) lds_barrier();
   if (lg == 0) {
 #pragma unroll
     for (int n = 0; n < TS; ++n)
 #pragma unroll
       for (int k = 0; k < 6; ++k) red[(wl * BM + (sbo + n) * 16 + lr) * 6 + k] = v[n * 6 + k];
   }
+  if (!PUBLISH) return;  // a later call on the tile's other sample blocks publishes
   lds_barrier();
   for (int r = tid; r < BM; r += NT) {
     const int s = s0 + r;
@@ -958,7 +1009,7 @@ MPV_DEV void fwd_tile_epilogue_t(const FwdParams& p, f32x4 (&acc)[TL][TS], float
 }
 
 // Column partials of a transposed-tile workgroup -> colpart[sc, ., b, n0 ...]
-template <int WS, int BN>
+template <int WS, int BN, int CQ = 1>
 MPV_DEV void fwd16t_colpart(const FwdParams& p, const float* cacc, int b, int sc, int n0,
                             int nthreads) {
   lds_barrier();
@@ -967,7 +1018,7 @@ MPV_DEV void fwd16t_colpart(const FwdParams& p, const float* cacc, int b, int sc
     if (l < p.L) {
       float e = 0.f, x = 0.f;
 #pragma unroll
-      for (int w = 0; w < WS; ++w) {
+      for (int w = 0; w < WS * CQ; ++w) {
         e += cacc[(w * BN + c) * 2 + 0];
         x += cacc[(w * BN + c) * 2 + 1];
       }
@@ -1168,6 +1219,207 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
     fwd16a_tiles<TSB, false, TSA, TSB, TL>(p, smem, red, cacc, cols, dma, true, b, nt, t_begin, t_end,
                                        nK, soft_any, wl, TSA, lr, coh, col, scale, prio1);
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
+}
+
+// ------------------ 3xf16, 256 labels x 256 samples (probit_fwd16b, study)
+// probit_fwd16a with twice the samples per tile: the stage image streams
+// (256 + 256) rows for 256 x 256 x 32 products instead of (256 + 128) for
+// 256 x 128 x 32 (a third fewer operand bytes per product), and each wave's
+// fragment reads cover 64 x TS*16 products.  The accumulators (TL x TSW
+// blocks) leave room for all R fragments of a stage but not all eps ones, so
+// the eps fragments of one 16-sample block are read right before its
+// products (one block ahead).  The row-statistics exchange (red, 24 KB)
+// lives in the stage image the tile's last K stage was read from.
+// Fwd16Dma for S >= BM (no row clamp): the pieces of one operand image are
+// 32 rows apart, and (r >> 1) & 7 repeats every 16 rows, so every piece of an
+// image has the same per-lane offset from its (wave-uniform) row base -- two
+// offset VGPRs instead of JA + JB.
+template <int BM, int BN, int NW>
+struct Fwd16DmaLin {
+  static constexpr int GA = BM / 8, GB = BN / 8;
+  static constexpr int JA = GA / NW, JB = GB / NW;
+  static_assert(GA % NW == 0 && GB % NW == 0, "pieces split evenly over the DMA waves");
+  const char* a_base;  // eps rows of the current tile, this wave's first piece
+  const char* b_base;  // R rows of the label tile, this wave's first piece
+  int64_t a_step, b_step;  // bytes between a wave's consecutive pieces (NW * 8 rows)
+  uint32_t offa, offb;
+  int tile, kc, issued, wid;
+
+  MPV_DEV void init(const FwdParams& p, int t0, int b, int n0, int wid_, int lane) {
+    wid = wid_;
+    const int64_t lda = p.eps16.ld, ldb = p.R16.ld;
+    const int prow = lane >> 3, u_lds = lane & 7;
+    a_step = (int64_t)NW * 8 * lda * 2;
+    b_step = (int64_t)NW * 8 * ldb * 2;
+    b_base = reinterpret_cast<const char*>(p.R16.data + ((int64_t)n0 + wid * 8) * ldb);
+    offa = (uint32_t)(prow * lda * 2) + (uint32_t)((u_lds ^ (((wid * 8 + prow) >> 1) & 7)) * 16);
+    offb = (uint32_t)(prow * ldb * 2) + (uint32_t)((u_lds ^ (((wid * 8 + prow) >> 1) & 7)) * 16);
+    tile = t0;
+    kc = 0;
+    issued = 0;
+    set_tile(p, b);
+  }
+  MPV_DEV void set_tile(const FwdParams& p, int b) {
+    const int64_t o = ((int64_t)b * p.S + fwd_tile_s0<BM>(tile, p.S) + wid * 8) * p.eps16.ld;
+    a_base = reinterpret_cast<const char*>(p.eps16.data + o);
+  }
+  MPV_DEV void issue(const FwdParams& p, char* dst, int tile_end, int nK, int b) {
+    if (tile >= tile_end) return;
+    const int kb = kc * kRowB;
+#pragma unroll
+    for (int j = 0; j < JA; ++j)
+      lds_dma16(a_base + kb + j * a_step, offa, lds_addr(dst + (wid + j * NW) * 1024));
+#pragma unroll
+    for (int j = 0; j < JB; ++j)
+      lds_dma16(b_base + kb + j * b_step, offb, lds_addr(dst + BM * kRowB + (wid + j * NW) * 1024));
+    ++issued;
+    if (++kc == nK) {
+      kc = 0;
+      if (++tile < tile_end) set_tile(p, b);
+    }
+  }
+};
+
+template <int TSW, int TL>
+MPV_DEV void fwd16b_stage(f32x4 (&acc)[TL][TSW], const char* base, int wl, int sbo, int lr, int coh,
+                          int col) {
+  constexpr int BM = 256;
+  s16x8 rh[TL], rl[TL];
+#pragma unroll
+  for (int m = 0; m < TL; ++m) {
+    const int off = (BM + (wl * TL + m) * 16 + lr) * kRowB;
+    rh[m] = *reinterpret_cast<const s16x8*>(base + off + coh);
+    rl[m] = *reinterpret_cast<const s16x8*>(base + off + col);
+  }
+  s16x8 eh = *reinterpret_cast<const s16x8*>(base + (sbo * 16 + lr) * kRowB + coh);
+  s16x8 el = *reinterpret_cast<const s16x8*>(base + (sbo * 16 + lr) * kRowB + col);
+#pragma unroll
+  for (int n = 0; n < TSW; ++n) {
+    s16x8 eh2, el2;
+    if (n + 1 < TSW) {  // the next block's fragments, in flight under these MFMAs
+      const int off = ((sbo + n + 1) * 16 + lr) * kRowB;
+      eh2 = *reinterpret_cast<const s16x8*>(base + off + coh);
+      el2 = *reinterpret_cast<const s16x8*>(base + off + col);
+    }
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rh[m]), as_f16x8(eh), acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rh[m]), as_f16x8(el), acc[m][n], 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+      acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(rl[m]), as_f16x8(eh), acc[m][n], 0, 0, 0);
+    if (n + 1 < TSW) {
+      eh = eh2;
+      el = el2;
+    }
+  }
+}
+
+template <int PART, int NP, int TL, int TSW, int BM>
+MPV_DEV void fwd16b_epilogue_parts(const FwdParams& p, f32x4 (&acc)[TL][TSW], float scale, int b, int s0,
+                                   int s_own, int nt, float* red, float* cacc, const float* cols,
+                                   bool soft_any, int sbo) {
+  constexpr int H0 = TSW / NP, H = PART + 1 < NP ? H0 : TSW - (NP - 1) * H0;  // the last takes the rest
+  static_assert(H0 >= 1, "a block per part at least");
+  f32x4 a[TL][H];
+#pragma unroll
+  for (int m = 0; m < TL; ++m)
+#pragma unroll
+    for (int n = 0; n < H; ++n) a[m][n] = acc[m][PART * H0 + n];
+  fwd_tile_epilogue_t<4, 2, TL, H, BM, PART == 0, kFwdBEpi, kFwdBUnroll, PART == NP - 1, kFwdBCQ>(
+      p, a, scale, b, s0, s_own, nt, red, cacc, cols, soft_any, sbo + PART * H0);
+  if constexpr (PART + 1 < NP)
+    fwd16b_epilogue_parts<PART + 1, NP, TL, TSW, BM>(p, acc, scale, b, s0, s_own, nt, red, cacc, cols,
+                                                     soft_any, sbo);
+}
+
+template <int TSW, int TSA, int TSB, int TL>
+MPV_DEV void fwd16b_tiles(const FwdParams& p, char* smem, float* cacc, const float* cols,
+                          Fwd16DmaLin<256, TL * 64, 4>& dma, bool dmaw, int b, int nt, int t_begin,
+                          int t_end, int nK, bool soft_any, int wl, int sbo, int lr, int coh, int col,
+                          float scale, bool prio1) {
+  constexpr int BM = 256, NSTAGE = 2;
+  constexpr int STAGE = (BM + TL * 64) * kRowB;
+  int gs = 0;
+  for (int st = t_begin; st < t_end; ++st) {
+    const int s0 = fwd_tile_s0<BM>(st, p.S);
+    f32x4 acc[TL][TSW];
+#pragma unroll
+    for (int m = 0; m < TL; ++m)
+#pragma unroll
+      for (int n = 0; n < TSW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < nK; ++kc, ++gs) {
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier_raw();  // stage gs landed for every wave; every wave is done reading gs-1
+      if (dmaw) {
+        dma.issue(p, smem + ((__builtin_amdgcn_readfirstlane(gs) + NSTAGE - 1) % NSTAGE) * STAGE,
+                  t_end, nK, b);
+      }
+      fwd16b_stage<TSW, TL>(acc, smem + (gs % NSTAGE) * STAGE, wl, sbo, lr, coh, col);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    // the image of stage gs-1 (read last) is free until the next tile's first
+    // barrier; stage gs streams into the other one meanwhile
+    float* red = reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
+    // in kFwdBParts parts of the wave's sample blocks (the row statistics of
+    // one part in registers at a time)
+    fwd16b_epilogue_parts<0, (TSW / kFwdBPart > 0 ? TSW / kFwdBPart : 1), TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc,
+                                                      cols, soft_any, sbo);
+    if (prio1)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+template <int TSA, int TSB, int TL>
+__global__ __launch_bounds__(512, 1) void probit_fwd16b_kernel(FwdParams p) {
+  constexpr int WL = 4, WS = 2, NW = 8, NSTAGE = 2;
+  constexpr int BM = (TSA + TSB) * 16, BN = WL * TL * 16;
+  static_assert(BM == 256, "the sample tile is 256");
+  constexpr int STAGE = (BM + BN) * kRowB;
+  static_assert(WL * BM * 6 * 4 <= STAGE, "red fits one stage image");
+  constexpr int CACC = WS * kFwdBCQ * BN * 2;  // floats
+  __shared__ __attribute__((aligned(1024))) char smem[NSTAGE * STAGE + (CACC + kColsT * BN) * 4];
+  float* cacc = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  float* cols = cacc + CACC;
+
+  int g, nt;
+  decode_block(blockIdx.x, p.B * p.nSc, p.nNt, g, nt);
+  const int b = g / p.nSc, sc = g % p.nSc;
+  const int n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = wid % WL;
+  const int lr = lane & 15, lg = lane >> 4;
+  const float scale = 1.0f / (*p.eps16.scale * *p.R16.scale);
+  const int nK = (p.z + kKC - 1) / kKC;
+  const int sw = (lr >> 1) & 7;
+  const int coh = (lg ^ sw) << 4, col = ((4 + lg) ^ sw) << 4;
+  const int t_begin = sc * p.tps, t_end = min(p.nSt, (sc + 1) * p.tps);
+
+  fwd_cols_stage_t<BN>(cols, p, b, n0, NW * 64);
+  for (int i = tid; i < CACC; i += NW * 64) cacc[i] = 0.0f;
+  const bool soft_any = fwd_tile_soft<BN>(p, b, n0, NW * 64);
+  const bool dmaw = wid >= NW / 2;  // the TSB half streams the stages
+  Fwd16DmaLin<BM, BN, NW / 2> dma;
+  dma.init(p, t_begin, b, n0, wid % (NW / 2), lane);
+  if (dmaw) {
+#pragma unroll
+    for (int j = 0; j < NSTAGE - 1; ++j) dma.issue(p, smem + j * STAGE, t_end, nK, b);
+  }
+  const bool prio1 = dmaw;
+  if (prio1) __builtin_amdgcn_s_setprio(1);
+  if (wid < NW / 2)
+    fwd16b_tiles<TSA, TSA, TSB, TL>(p, smem, cacc, cols, dma, false, b, nt, t_begin, t_end, nK,
+                                    soft_any, wl, 0, lr, coh, col, scale, prio1);
+  else
+    fwd16b_tiles<TSB, TSA, TSB, TL>(p, smem, cacc, cols, dma, true, b, nt, t_begin, t_end, nK,
+                                    soft_any, wl, TSA, lr, coh, col, scale, prio1);
+  fwd16t_colpart<WS, BN, kFwdBCQ>(p, cacc, b, sc, n0, NW * 64);
 }
 
 // The six scalars of compute_loss (mpvae.py:147-148 KL, :188-190 nll, :122
@@ -1394,7 +1646,14 @@ static FwdPlan plan_fwd(const mpv_shape* s, int gemm) {
   // transposed 96-label tile is the one used now.)
   const bool f16 = gemm == MPV_GEMM_F16X3;
   pl.cfg = s->L <= 48 ? 0 : (s->L <= 96 ? 1 : ((f16 && s->L > 128) ? 3 : 2));
-  pl.BM = (f16 && pl.cfg == 0) ? kFwd48BM : 128;
+  // (the 256 x 256 tile streams whole tiles: S >= 256, Fwd16DmaLin.
+  // MPVAE_FWD_TILE=256x128 selects round 5's tile instead: a diagnostic for
+  // the tests that compare the two, not a tuning knob)
+  const char* tile_env = std::getenv("MPVAE_FWD_TILE");
+  const bool tile128 = tile_env != nullptr && std::strcmp(tile_env, "256x128") == 0;
+  pl.BM = (f16 && pl.cfg == 0) ? kFwd48BM
+                               : ((f16 && pl.cfg == 3 && kFwdB && !tile128 && s->S_local >= 256) ? 256
+                                                                                                 : 128);
   pl.BN = pl.cfg == 0 ? 48 : (pl.cfg == 1 ? 96 : (pl.cfg == 2 ? 128 : 256));
   pl.nNt = (int)cdiv(s->L, pl.BN);
   pl.nSt = (int)cdiv(s->S_local, pl.BM);
@@ -1433,7 +1692,10 @@ static void launch_fwd(const FwdPlan& pl, int gemm, dim3 grid, hipStream_t st, c
                    dim3(512), 0, st, p);
         break;
       case 3:  // 256 labels x 128 samples, 8 waves, asymmetric 80 / 48 sample split
-        MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3, 4>), grid, dim3(512), 0, st, p);
+        if (pl.BM == 256)
+          MPV_LAUNCH("probit_fwd", (probit_fwd16b_kernel<kFwdBA, 16 - kFwdBA, 4>), grid, dim3(512), 0, st, p);
+        else
+          MPV_LAUNCH("probit_fwd", (probit_fwd16a_kernel<5, 3, 4>), grid, dim3(512), 0, st, p);
         break;
       case 1:  // 96 labels x 128 samples (48 < L <= 96), 8 waves of 48 x 32, even split
         MPV_LAUNCH("probit_fwd", (probit_fwd16t_kernel<2, 4, 3, 2, 2>), grid, dim3(512), 0, st, p);

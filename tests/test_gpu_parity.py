@@ -274,6 +274,8 @@ RANDOM_CASES = [
     (700, 64, 3, 130, 8),        # 512 < L < 1024: ring element pass with masked waves
     (1024, 1000, 2, 300, 8),     # 256-label tiles: 3 sample tiles, ragged K
     (260, 1024, 3, 257, 8),      # 256-label tiles, pad labels in the last label tile
+    (300, 200, 2, 255, 8),       # S < 256: the 256 x 128 tile
+    (260, 64, 2, 256, 8),        # S = 256: one 256 x 256 tile per label tile
     # tile boundaries of round 3: forward 48 / 96 / 128-label tiles, dR 64 / 128 tiles
     (48, 64, 4, 150, 8),         # last L of the 48-label tile; 64 x 64 dR tile at its edge
     (49, 65, 4, 150, 8),         # first L of the 96-label tile; z = 65: 128 dR tile
@@ -903,6 +905,41 @@ def test_forward_statistics_bitwise_repeatable(B, S, L, z):
         for name, a, b in zip(names, got, first):
             bad = int((a != b).sum())
             assert bad == 0, (name, bad)
+
+
+@pytest.mark.parametrize("B,S,L,z", [(8, 4096, 1024, 1024), (3, 700, 300, 200), (2, 256, 260, 64)],
+                         ids=["c4dims", "ragged", "s256"])
+def test_256x256_tile_equals_256x128_tile(B, S, L, z, monkeypatch):
+    """The shipped 256-label x 256-sample forward tile (probit_fwd16b, S >= 256)
+    and round 5's 256 x 128 tile (probit_fwd16a, still dispatched for S < 256,
+    where the probit sweep of test_gpu_probit_ulp.py runs) compute every t
+    with the same MFMA sequence and the same epilogue code, so T, the per-sample
+    statistics and the batch statistics agree bit for bit; only the column
+    sums over samples are added in another order (lane quads)."""
+    g = torch.Generator(device=DEV).manual_seed(B * 7 + S)
+    y = (torch.rand((B, L), device=DEV, generator=g) < 0.15).float()
+    y[:, 0], y[:, 1] = 1, 0
+    fe = torch.randn((B, L), device=DEV, generator=g)
+    fx = torch.randn((B, L), device=DEV, generator=g)
+    R = (torch.rand((L, z), device=DEV, generator=g, dtype=torch.float64) * 2 - 1) * 0.05
+    be = HipShardBackend(poison=True)
+    shape = be.shape(S, S, 0, B, L, z)
+    Rop = be.prepare_R(R)
+    eps = be.make_noise(shape, DEV, 77, 0)
+    outs = {}
+    for tile in ("256x256", "256x128"):
+        if tile == "256x128":
+            monkeypatch.setenv("MPVAE_FWD_TILE", "256x128")
+        loc = be.forward_local(shape, y, fe, fx, Rop, eps, keep_T=True)
+        torch.cuda.synchronize()
+        outs[tile] = {k: loc[k].clone() for k in ("rowstat", "bstat", "colsum")}
+        outs[tile]["T"] = loc["T"][..., :L].clone()
+    a, b = outs["256x256"], outs["256x128"]
+    for k in ("T", "rowstat", "bstat"):
+        assert torch.equal(a[k], b[k]), (k, int((a[k] != b[k]).sum()))
+    assert torch.isfinite(a["colsum"]).all()
+    err = ((a["colsum"] - b["colsum"]).abs().max() / b["colsum"].abs().max()).item()
+    assert err <= 1e-6, err
 
 
 def test_gemm_modes_agree_at_c4_dims():
