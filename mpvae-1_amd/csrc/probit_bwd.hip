@@ -37,9 +37,12 @@ int launch_sum_slabs_pair(const float* in0, int64_t nslab0, int64_t n0, void* ou
 constexpr float kBoundDl = 4.5f, kBoundPos = 0.4f, kBoundNeg = 60.0f, kBoundInd = 0.4f;
 
 // --------------------------------------------------------------- coefficients
-// bwd_coef: one workgroup per batch row (512 or 256 threads: C2 -1.7 / +0 us,
-// C3 +-0 / +2 us, C4 +-0 / +3 us; round 3, same box)
-constexpr int kCoefThreads = 1024;
+// bwd_coef: one workgroup per batch row of 512 threads (1024: C2 +1.3 us, C3
+// +-0, round 6; 256: C2 +1.7, C3 +2, C4 +3 us against 512, round 3)
+#ifndef MPV_COEF_THREADS
+#define MPV_COEF_THREADS 512
+#endif
+constexpr int kCoefThreads = MPV_COEF_THREADS;
 
 __global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
     const float* __restrict__ y, const float* __restrict__ rowstat, const float* __restrict__ bstat,
@@ -1227,6 +1230,11 @@ static BwdPlan plan_bwd(const mpv_shape* s, int gemm) {
   // kElemRingMinRows, which matters at small n_sample: the strong-scaling share)
   const int64_t min_rows = (planes && pl.RPI == 1) ? kElemRingMinRows : kElemMinRows;
   want = std::min<int64_t>(want, cdiv(S, (int64_t)pl.RPI * min_rows));
+  // but two blocks per CU at least when a thread still gets kElemMinRows / 2
+  // rows (C2: 384 blocks, 1.5 per CU, left half the CUs with one wave per
+  // SIMD: element pass 24.9 -> 22.3 us with 512; C3 has 2816 either way)
+  const int64_t even = cdiv(2 * (int64_t)num_cus(), B * pl.nLc);
+  if (want < even && cdiv(S, even * pl.RPI) >= kElemMinRows / 2) want = even;
   if (want < 1) want = 1;
   const int64_t max_chunks = cdiv(S, pl.RPI);
   if (want > max_chunks) want = max_chunks;

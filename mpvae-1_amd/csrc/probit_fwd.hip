@@ -52,7 +52,10 @@ struct FwdParams {
 // lists the variants that lost and were removed):
 // fwd_combine: one block per batch row (512 / 256 threads: C4 0.076 -> 0.115 /
 // 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3)
-constexpr int kCombineThreads = 1024;
+#ifndef MPV_COMBINE_THREADS
+#define MPV_COMBINE_THREADS 1024
+#endif
+constexpr int kCombineThreads = MPV_COMBINE_THREADS;
 constexpr int kCombineFoldSlabs = 64;  // s-chunk partials fwd_combine sums itself, at most
 constexpr int kCombineKeep = 4;        // fwd_combine: samples per thread kept in registers
 constexpr int kFwdWant = 2048;         // fp32 mode: target workgroup count of the forward grid

@@ -401,6 +401,10 @@ constexpr float kNoiseScale = 4096.0f;
 // the block several rows at once.
 constexpr int kNoiseRows = 16;  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
 constexpr int kNoiseCols = 8;   // plane columns per thread (4: 1.78 ms, 8: 1.69 ms at C4)
+#ifndef MPV_NOISE_PASSES
+#define MPV_NOISE_PASSES 2
+#endif
+constexpr int kNoisePasses = MPV_NOISE_PASSES;  // narrow planes: row passes per block
 // Plane columns the noise kernel writes: z rounded up to the GEMMs' 32-wide K
 // slices (zeros past z).  Columns beyond that (the dR tile's padding) are left
 // as they are: the forward GEMM never reads them, and in the dR GEMM they only
@@ -459,6 +463,19 @@ MPV_DEV void noise16_oct(int64_t e_row, int c0, int z, uint64_t offset, uint32_t
   }
 }
 
+// Lanes per plane row of a narrow plane: the 8-column groups that hold normals.
+__host__ __device__ inline int noise_narrow_tpr(int z) { return (z + kNoiseCols - 1) / kNoiseCols; }
+
+// Zero columns c_first .. cols-1 (whole 8-column groups) of plane row r.
+template <int CPT>
+MPV_DEV void noise16_zero_tail(const mpv_split16& out, int r, int c_first, int cols) {
+  for (int c0 = c_first; c0 < cols; c0 += CPT) {
+    const int64_t o = chunked_index(r, out.ld, c0);
+    *reinterpret_cast<s16x8*>(out.data + o) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    *reinterpret_cast<s16x8*>(out.data + o + kLoOff) = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+
 // Columns c_first, c_first + c_step, ... (CPT each, two 16-B stores) of
 // plane row r.
 template <int CPT>
@@ -488,7 +505,7 @@ MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_
 __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, int S, int B,
                                                             int z, int64_t s_off, uint32_t k0,
                                                             uint32_t k1, uint64_t offset,
-                                                            int rows,
+                                                            int rows, int rpb,
                                                             const uint64_t* __restrict__ seed_dev,
                                                             SmallSplit ss) {
   // r_sqrt_sigma's split, beside the noise (one launch): the first workgroups,
@@ -508,19 +525,24 @@ __global__ __launch_bounds__(256) void noise_philox16_kernel(mpv_split16 out, in
   // run after this kernel)
   if (nblk == 0 && threadIdx.x == 0) *out.scale = kNoiseScale;
   const int cols = noise_written_cols(out, z);
-  const int r_end = min(rows, (int)(nblk + 1) * kNoiseRows);
+  const int r_end = min(rows, (int)(nblk + 1) * rpb);
   constexpr int CPT = kNoiseCols;
-  const int tpr = min((int)blockDim.x, cols / CPT);  // threads per row
-  if (tpr == (int)blockDim.x) {  // wide planes: the row (and its index math) is block-uniform
-    for (int r = nblk * kNoiseRows; r < r_end; ++r)
+  if (cols / CPT >= (int)blockDim.x) {  // wide planes: the row (and its index math) is block-uniform
+    for (int r = nblk * rpb; r < r_end; ++r)
       noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, threadIdx.x * CPT,
                        blockDim.x * CPT);
-  } else {  // narrow planes (C2, C3): several rows per pass of the block
+  } else {
+    // narrow planes (C2, C3): a lane per 8 columns holding normals (the zero
+    // columns z .. cols-1 past them are stored by the row's last lane, not
+    // given lanes of their own), several rows per pass of the block
+    const int tpr = noise_narrow_tpr(z);
     const int rpi = (int)blockDim.x / tpr;
     if ((int)threadIdx.x >= rpi * tpr) return;
-    for (int r = nblk * kNoiseRows + (int)threadIdx.x / tpr; r < r_end; r += rpi)
-      noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, ((int)threadIdx.x % tpr) * CPT,
-                       tpr * CPT);
+    const int t = (int)threadIdx.x % tpr;
+    for (int r = nblk * rpb + (int)threadIdx.x / tpr; r < r_end; r += rpi) {
+      noise16_row<CPT>(out, S, B, z, s_off, k0, k1, offset, r, t * CPT, cols);
+      if (t == tpr - 1) noise16_zero_tail<CPT>(out, r, tpr * CPT, cols);
+    }
   }
 }
 
@@ -662,16 +684,22 @@ static int noise_philox_f16(const mpv_shape* shape, uint64_t seed, const uint64_
   hipStream_t s = as_stream(stream);
   MPV_REQUIRE(rows < (int64_t(1) << 31) && shape->z < (int64_t(1) << 31), "noise too large");
   const int64_t tpr = noise_written_cols(*out, (int)shape->z) / kNoiseCols;  // threads per plane row
-  const unsigned threads = tpr >= 256 ? 256 : (unsigned)(cdiv(tpr, 64) * 64);
+  // narrow planes (fewer than 256 8-column groups per row): 256-thread blocks
+  // of several rows per pass, kNoisePasses passes (short one-wave blocks were
+  // dispatch-bound at C2)
+  const bool narrow = tpr < 256 && !(tpr % 64 == 0);
+  const unsigned threads = narrow || tpr >= 256 ? 256 : (unsigned)tpr;
+  int rpb = kNoiseRows;
+  if (narrow) rpb = (256 / noise_narrow_tpr((int)shape->z)) * kNoisePasses;
   if (ss.x != nullptr) {
     const int64_t plane_elems = ss.out.rows_pad * (ss.out.ld / 2);
     ss.nblocks = (int)std::min<int64_t>(cdiv(plane_elems, (int64_t)threads * 8), 64);
   }
-  const int64_t nb = cdiv(rows, kNoiseRows) + ss.nblocks;
+  const int64_t nb = cdiv(rows, rpb) + ss.nblocks;
   MPV_REQUIRE(nb < (int64_t(1) << 31), "noise grid too large");
   MPV_LAUNCH("noise_philox", noise_philox16_kernel, dim3((unsigned)nb), dim3(threads), 0, s, *out,
              (int)shape->S_local, (int)shape->B, (int)shape->z, shape->s_offset, (uint32_t)seed,
-             (uint32_t)(seed >> 32), offset, (int)rows, seed_dev, ss);
+             (uint32_t)(seed >> 32), offset, (int)rows, rpb, seed_dev, ss);
   return check_launch("noise_philox_f16");
 }
 
