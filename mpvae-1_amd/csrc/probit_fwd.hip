@@ -1429,7 +1429,10 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16b_kernel(FwdParams p) {
 // ranking mean, :207-208 total) from the per-row statistics, by ONE block of
 // kFinalThreads threads.  row(b, v) yields row b's (M, Z, M_x, Z_x, c, c_x);
 // both finalize variants sum in this same order.
-constexpr int kFinalThreads = 1024;
+#ifndef MPV_FINAL_THREADS
+#define MPV_FINAL_THREADS 1024
+#endif
+constexpr int kFinalThreads = MPV_FINAL_THREADS;
 template <class Row>
 MPV_DEV void finalize_scalars(const mpv_final_args& a, int B, float S_total, Row row) {
   __shared__ float red[16 * 5];
@@ -1761,7 +1764,7 @@ template <bool SLOTS>
 static int launch_finalize(const mpv_shape* shape, const mpv_final_args& a, int nslots,
                            float* bstat_out, hipStream_t st) {
   const int64_t n = shape->B * shape->L;
-  int64_t nb = cdiv(n, 1024);
+  int64_t nb = cdiv(n, kFinalThreads);
   if (nb > 2048) nb = 2048;
   MPV_LAUNCH("finalize", finalize_kernel<SLOTS>, dim3((unsigned)(1 + nb)), dim3(kFinalThreads), 0,
              st, a, (int)shape->B, (int)shape->L, (float)shape->S_total, nslots, bstat_out);
