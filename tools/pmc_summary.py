@@ -10,7 +10,8 @@ the bytes of a wide (16 B/lane) coalesced read -> x2; WRITE_SIZE is exact for
 summarised here are 16 B/lane (float4) except where noted in DESIGN.md.
 
 A `valu` pass (tools/profile.sh STEPS=valu: SQ_INSTS_VALU, SQ_INSTS_MFMA,
-GRBM_GUI_ACTIVE), when present, adds per kernel the VALU lane-instructions per
+SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE), when present, adds per kernel the
+MFMA-busy fraction of the SIMDs' cycles, the VALU lane-instructions per
 launch ((SQ_INSTS_VALU - SQ_INSTS_MFMA) x 64: wave-instructions of 64 lanes;
 the counter counts MFMAs as VALU) and the effective clock (GRBM_GUI_ACTIVE / 8
 XCDs / trace duration), and the whole step's VALU lane-instructions -- bench.py
@@ -81,6 +82,7 @@ def main(src, dst, tag):
     write = opt("write", "WRITE_SIZE")
     valu, mfma, grbm = opt("valu", "SQ_INSTS_VALU"), opt("valu", "SQ_INSTS_MFMA"), \
         opt("valu", "GRBM_GUI_ACTIVE")
+    mbusy = opt("valu", "SQ_VALU_MFMA_BUSY_CYCLES")
     out = {"source": src, "note": "bytes per launch; fetch corrected x2 (gfx950 FETCH_SIZE "
                                   "reports half of 16B/lane reads)", "kernels": {}}
     for k in sorted(set(fetch) | set(write) | set(valu)):
@@ -100,6 +102,10 @@ def main(src, dst, tag):
             out["kernels"][k].update(
                 valu_lane_insts_per_launch=lanes, mfma_insts_per_launch=mfma.get(k),
                 clock_ghz=(grbm[k] / 8.0 / (d * 1e6) if k in grbm and d else None))
+            if k in mbusy and k in grbm:
+                # MFMA-busy cycles per SIMD (1024 SIMDs) over the kernel's GPU cycles
+                # (GRBM_GUI_ACTIVE summed over the 8 XCDs)
+                out["kernels"][k]["mfma_busy_frac"] = mbusy[k] / 1024.0 / (grbm[k] / 8.0)
     # aliases under the timing tags bench.py reports (e.g. probit_fwd16 -> probit_fwd)
     for k in list(out["kernels"]):
         t = tag_of(k)

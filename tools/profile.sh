@@ -27,7 +27,7 @@ for s in $STEPS; do
     trace) run trace --kernel-trace --stats ;;
     fetch) run fetch --pmc FETCH_SIZE --kernel-include-regex "$KRE" ;;
     write) run write --pmc WRITE_SIZE --kernel-include-regex "$KRE" ;;
-    valu) run valu --pmc SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-include-regex "${VKRE:-mpv::}" ;;
+    valu) run valu --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "${VKRE:-mpv::}" ;;
   esac
 done
 find "$OUT" -name "*.csv" | head -20
