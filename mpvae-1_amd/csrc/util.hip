@@ -309,6 +309,81 @@ __global__ __launch_bounds__(256) void maxabs_kernel(const T* __restrict__ x, in
 }
 
 
+// maxabs_kernel on 16-B vectors with four independent maxima per thread (the
+// scalar loop kept a dependent max chain and few loads in flight: 10.6 us for
+// r_sqrt_sigma at C4).  x 16-B aligned; the n % VEC tail is block 0's.
+template <typename T>
+__global__ __launch_bounds__(256) void maxabs_vec_kernel(const T* __restrict__ x, int64_t n,
+                                                        float* __restrict__ block_max) {
+  constexpr int VEC = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(VEC)));
+  __shared__ float red[16];
+  const vec_t* xv = reinterpret_cast<const vec_t*>(x);
+  const int64_t nv = n / VEC, st = (int64_t)gridDim.x * blockDim.x;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * st < nv; i += 4 * st) {
+    const vec_t a = xv[i], b = xv[i + st], c = xv[i + 2 * st], d = xv[i + 3 * st];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      m0 = fmaxf(m0, fabsf((float)a[k]));
+      m1 = fmaxf(m1, fabsf((float)b[k]));
+      m2 = fmaxf(m2, fabsf((float)c[k]));
+      m3 = fmaxf(m3, fabsf((float)d[k]));
+    }
+  }
+  for (; i < nv; i += st) {
+    const vec_t a = xv[i];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) m0 = fmaxf(m0, fabsf((float)a[k]));
+  }
+  if (blockIdx.x == 0)
+    for (int64_t j = nv * VEC + threadIdx.x; j < n; j += blockDim.x) m1 = fmaxf(m1, fabsf((float)x[j]));
+  float m = block_reduce<true>(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), red);
+  if (threadIdx.x == 0) block_max[blockIdx.x] = m;
+}
+
+// split_kernel for cols % 8 == 0 and a 16-B aligned x: a thread splits 8
+// consecutive columns of one row (vector loads) and writes their hi and lo
+// halves as two 16-B stores (the scalar kernel's 2-B stores: 7.5 us for
+// r_sqrt_sigma at C4).  Same values as split_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void split8_kernel(const T* __restrict__ x, int64_t rows,
+                                                    int64_t cols, mpv_split16 out,
+                                                    const float* __restrict__ bmax, int nb) {
+  constexpr int VEC = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(VEC)));
+  const float s = wave_pow2_scale(bmax, nb);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out.scale = s;
+  const int64_t g8 = (out.ld >> 1) / 8;  // 8-column groups per plane row
+  const int64_t n = out.rows_pad * g8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / g8, c0 = (i - r * g8) * 8;
+    float v[8];
+    if (r < rows && c0 < cols) {  // cols % 8 == 0: all 8 columns are in range
+      const vec_t* xv = reinterpret_cast<const vec_t*>(x + r * cols + c0);
+#pragma unroll
+      for (int q = 0; q < 8 / VEC; ++q) {
+        const vec_t a = xv[q];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[q * VEC + k] = (float)a[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = 0.0f;
+    }
+    uint16_t h[8], l[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) split_f16(v[k], s, h[k], l[k]);
+    const int64_t o = chunked_index(r, out.ld, c0);
+    *reinterpret_cast<s16x8*>(out.data + o) =
+        s16x8{(short)h[0], (short)h[1], (short)h[2], (short)h[3], (short)h[4], (short)h[5], (short)h[6], (short)h[7]};
+    *reinterpret_cast<s16x8*>(out.data + o + kLoOff) =
+        s16x8{(short)l[0], (short)l[1], (short)l[2], (short)l[3], (short)l[4], (short)l[5], (short)l[6], (short)l[7]};
+  }
+}
+
 // (rows, cols) row-major -> chunked split planes (rows_pad x ld/2 columns),
 // zero padded.  Thread i owns logical element (r, c) = (i / cols_pad, i % cols_pad).
 // The scale comes from the nb block maxima of maxabs_kernel, taken by every
@@ -660,12 +735,28 @@ int mpv_split_f16(const void* x, int x_dtype, int64_t rows, int64_t cols, const 
   float* bmax = reinterpret_cast<float*>(workspace);
   const int64_t n = rows * cols;
   const unsigned g = grid_for(n, 256, kSplitMaxBlocks);
-  if (x_dtype == MPV_F64)
+  const bool aligned = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const bool f64 = x_dtype == MPV_F64;
+  if (aligned && f64)
+    MPV_LAUNCH("split", maxabs_vec_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)x, n, bmax);
+  else if (aligned)
+    MPV_LAUNCH("split", maxabs_vec_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, n, bmax);
+  else if (f64)
     MPV_LAUNCH("split", maxabs_kernel<double>, dim3(g), dim3(256), 0, s, (const double*)x, n, bmax);
   else
     MPV_LAUNCH("split", maxabs_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, n, bmax);
+  if (aligned && cols % 8 == 0) {  // whole 8-column groups: vector loads, 16-B stores
+    const unsigned g2 = grid_for(out->rows_pad * (out->ld / 2) / 8, 256, 16384);
+    if (f64)
+      MPV_LAUNCH("split", split8_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)x, rows,
+                 cols, *out, bmax, (int)g);
+    else
+      MPV_LAUNCH("split", split8_kernel<float>, dim3(g2), dim3(256), 0, s, (const float*)x, rows,
+                 cols, *out, bmax, (int)g);
+    return check_launch("split_f16");
+  }
   const unsigned g2 = grid_for(out->rows_pad * (out->ld / 2), 256, 16384);
-  if (x_dtype == MPV_F64)
+  if (f64)
     MPV_LAUNCH("split", split_kernel<double>, dim3(g2), dim3(256), 0, s, (const double*)x, rows,
                cols, *out, bmax, (int)g);
   else
