@@ -190,6 +190,7 @@ struct SlabSum {
   void* out;
   int f64;     // out is double
   int split;   // the split layout (few columns, many slabs)
+  int vec;     // 4 consecutive elements per thread (16-B loads): n % 4 == 0, aligned
   int64_t blocks;
 };
 
@@ -220,6 +221,15 @@ __global__ __launch_bounds__(1024) void sum_slabs_pair_kernel(SlabSum a, SlabSum
 #pragma unroll
       for (int j = 1; j < 16; ++j) t += part[j][lane];
       slab_store(q, i, t);
+    }
+  } else if (q.vec) {  // the same sums, four elements per thread (16-B loads)
+    const int64_t i = (blk * 1024 + threadIdx.x) * 4;
+    if (i < q.n) {
+      f32x4 acc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int64_t k = 0; k < q.nslab; ++k) acc += *reinterpret_cast<const f32x4*>(q.in + k * q.n + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) slab_store(q, i + j, acc[j]);
     }
   } else {
     const int64_t i = blk * 1024 + threadIdx.x;
@@ -897,7 +907,8 @@ static SlabSum slab_problem(const float* in, int64_t nslab, int64_t n, void* out
   q.out = out;
   q.f64 = out_dtype == MPV_F64;
   q.split = nslab >= 64 && n <= 256 * 256;  // the rule of launch_sum_slabs
-  q.blocks = q.split ? cdiv(n, 64) : cdiv(n, 1024);
+  q.vec = !q.split && n % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+  q.blocks = q.split ? cdiv(n, 64) : (q.vec ? cdiv(n, 4096) : cdiv(n, 1024));
   return q;
 }
 
