@@ -1553,10 +1553,39 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
     l0 = v[0];
     l1 = v[1];
   };
+  // S % 4 == 0: the kept samples are four consecutive ones per thread, read
+  // and written as 16-B vectors (rowpart is 200 MB per launch at C4)
+  const bool vec = kCombineKeep == 4 && (S & 3) == 0;
+  if (vec) {
+    const int s0 = 4 * tid;
+    if (s0 < S) {
+      f32x4 v[6];
 #pragma unroll
-  for (int j = 0; j < kCombineKeep; ++j) {
-    const int s = tid + j * (int)blockDim.x;
-    if (s < S) sample(s, keep0[j], keep1[j]);
+      for (int k = 0; k < 6; ++k) {
+        f32x4 a{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < nNt; ++nt)
+          a += *reinterpret_cast<const f32x4*>(rowpart + (((int64_t)k * nNt + nt) * B + b) * S + s0);
+        v[k] = a;
+        *reinterpret_cast<f32x4*>(rowstat + ((int64_t)k * B + b) * S + s0) = a;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        me = fmaxf(me, v[0][j]);
+        mx = fmaxf(mx, v[1][j]);
+        const float le = (v[2][j] * v[3][j]) / (5.0f * nrm);
+        const float lx = (v[4][j] * v[5][j]) / (5.0f * nrm);
+        ce += isfinite(le) ? le : 0.0f;
+        cx += isfinite(lx) ? lx : 0.0f;
+        keep0[j] = v[0][j];
+        keep1[j] = v[1][j];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kCombineKeep; ++j) {
+      const int s = tid + j * (int)blockDim.x;
+      if (s < S) sample(s, keep0[j], keep1[j]);
+    }
   }
   for (int s = tid + kCombineKeep * (int)blockDim.x; s < S; s += blockDim.x) {
     float l0, l1;
@@ -1584,7 +1613,7 @@ __global__ __launch_bounds__(kCombineThreads) void fwd_combine_kernel(const floa
   float ze = 0.f, zx = 0.f;
 #pragma unroll
   for (int j = 0; j < kCombineKeep; ++j) {
-    const int s = tid + j * (int)blockDim.x;
+    const int s = vec ? 4 * tid + j : tid + j * (int)blockDim.x;
     if (s < S) {
       ze += expf(keep0[j] - me);
       zx += expf(keep1[j] - mx);
