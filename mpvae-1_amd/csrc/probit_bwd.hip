@@ -97,20 +97,38 @@ __global__ __launch_bounds__(kCoefThreads) void bwd_coef_kernel(
     const bool dead = !(nrm > 0.0f) && clive[br];
     const float cs = gc[br] / (nrm * S_total * (float)B);
     float bmax = 0.0f;
-    for (int s = tid; s < S; s += blockDim.x) {
-      const float lp = rowstat[((int64_t)br * B + b) * S + s];
-      const float P = rowstat[((int64_t)(2 + 2 * br) * B + b) * S + s];
-      const float N = rowstat[((int64_t)(3 + 2 * br) * B + b) * S + s];
+    // one sample's coefficients (stored times dE/du's constant kPhiK: the
+    // element pass then multiplies by exp(-u^2/2) alone)
+    auto one = [&](float lp, float P, float N, float& ca, float& cp, float& cn) {
       float alpha = -gn[br] * (expf(lp - M) / Z) * inv_B;
       float bP = nrm > 0.0f ? cs * N : 0.0f;
       float bN = nrm > 0.0f ? cs * P : 0.0f;
       bmax = fmaxf(bmax, kBoundDl * fabsf(alpha) + kBoundPos * fabsf(bP) + kBoundNeg * fabsf(bN));
       if (dead) alpha = bP = bN = __builtin_nanf("");
-      // stored times dE/du's constant kPhiK (the element pass then multiplies
-      // by exp(-u^2/2) alone)
-      coef[((int64_t)(3 * br + 0) * B + b) * S + s] = alpha * kPhiK;
-      coef[((int64_t)(3 * br + 1) * B + b) * S + s] = bP * kPhiK;
-      coef[((int64_t)(3 * br + 2) * B + b) * S + s] = bN * kPhiK;
+      ca = alpha * kPhiK;
+      cp = bP * kPhiK;
+      cn = bN * kPhiK;
+    };
+    const float* rl = rowstat + ((int64_t)br * B + b) * S;
+    const float* rp = rowstat + ((int64_t)(2 + 2 * br) * B + b) * S;
+    const float* rn = rowstat + ((int64_t)(3 + 2 * br) * B + b) * S;
+    float* ca = coef + ((int64_t)(3 * br + 0) * B + b) * S;
+    float* cp = coef + ((int64_t)(3 * br + 1) * B + b) * S;
+    float* cn = coef + ((int64_t)(3 * br + 2) * B + b) * S;
+    if ((S & 3) == 0) {  // four consecutive samples per thread, 16-B accesses (same values)
+      for (int s = 4 * tid; s < S; s += 4 * (int)blockDim.x) {
+        const f32x4 lp = *reinterpret_cast<const f32x4*>(rl + s);
+        const f32x4 P = *reinterpret_cast<const f32x4*>(rp + s);
+        const f32x4 N = *reinterpret_cast<const f32x4*>(rn + s);
+        float a[4], p[4], n[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) one(lp[j], P[j], N[j], a[j], p[j], n[j]);
+        *reinterpret_cast<f32x4*>(ca + s) = f32x4{a[0], a[1], a[2], a[3]};
+        *reinterpret_cast<f32x4*>(cp + s) = f32x4{p[0], p[1], p[2], p[3]};
+        *reinterpret_cast<f32x4*>(cn + s) = f32x4{n[0], n[1], n[2], n[3]};
+      }
+    } else {
+      for (int s = tid; s < S; s += blockDim.x) one(rl[s], rp[s], rn[s], ca[s], cp[s], cn[s]);
     }
     bmaxb[br] = bmax;
   }
