@@ -244,6 +244,26 @@ def test_seed_advance_in_finalize():
         mpvae.compute_loss(y, *base, mk(777, True))
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32], ids=["f64", "f32"])
+@pytest.mark.parametrize("cols,misalign", [(136, False), (130, False), (136, True)],
+                         ids=["vector", "ragged", "misaligned"])
+def test_large_split_paths(dtype, cols, misalign):
+    """mpv_split_f16 above the small-operand size: the 16-B vector kernels
+    (cols % 8 == 0, 16-B aligned input) and the scalar ones give the same
+    planes -- hi + lo == x to ~2^-22, zero padding, power-of-two scale."""
+    be = HipShardBackend("f16x3")
+    g = torch.Generator(device=DEV).manual_seed(cols)
+    rows = 300
+    flat = torch.randn(rows * cols + 1, device=DEV, dtype=dtype, generator=g) * 0.3
+    R = (flat[1:] if misalign else flat[:-1]).view(rows, cols)
+    pl = be.prepare_R(R)
+    v = pl.value().double()
+    err = (v[:rows, :cols] - R.double()).abs().max() / R.double().abs().max()
+    assert float(err) < 1e-6, float(err)
+    assert float(v[rows:].abs().max()) == 0.0 and float(v[:, cols:].abs().max()) == 0.0
+    assert 2 ** 13 <= float(R.abs().max()) * float(pl.scale) < 2 ** 14
+
+
 def test_split_planes_round_trip():
     """mpv_split_f16: power-of-two scale from max|x|, hi+lo == x to ~2^-22."""
     be = HipShardBackend("f16x3")
