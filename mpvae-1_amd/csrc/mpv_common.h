@@ -176,6 +176,13 @@ constexpr float kPhiK = kC1 * kInvSqrt2Pi;  // dE/du = kPhiK exp(-u^2/2)
 // zq = u sqrt(log2 e) / sqrt 2 is the caller's: it keeps u's sign (used only
 // squared, through |zq| as an fma abs source modifier, and for erf's sign),
 // and a caller with u = t + base forms it as one fma(t, kZq, base kZq).
+// 1 - erfc as one fma of the unrounded product (erfc is never formed): one
+// packed op fewer per element pair in the forward epilogue and the element
+// pass (forward -0.7 %, element pass -1.7 %, round 6), and the probit sweep's
+// per-band bounds unchanged (tests/test_gpu_probit_ulp.py)
+#ifndef MPV_OM_FMA
+#define MPV_OM_FMA 1
+#endif
 constexpr int kErfcDeg = 6;
 constexpr float kSqL2e = 1.2011224087864498f;  // sqrt(log2 e)
 constexpr float kZq = kInvSqrt2 * kSqL2e;
@@ -201,8 +208,12 @@ MPV_DEV void probit_w2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N]) {
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const f32x2 a = pk_fma(-zq[j], zq[j], p[j]);
-    const f32x2 erfc = t[j] * f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-    const f32x2 om = splat2(1.0f) - erfc;
+    const f32x2 e = f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+#if MPV_OM_FMA
+    const f32x2 om = pk_fma(-t[j], e, splat2(1.0f));  // 1 - erfc, erfc = t e unrounded
+#else
+    const f32x2 om = splat2(1.0f) - t[j] * e;
+#endif
     w[j] = splat2(1.0f) +
            f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};
   }
@@ -250,7 +261,11 @@ MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&ezo)[N
     const f32x2 az = -zq[j] * zq[j];
     const f32x2 ez = f32x2{__builtin_amdgcn_exp2f(az.x), __builtin_amdgcn_exp2f(az.y)};
     ezo[j] = ez;
+#if MPV_OM_FMA
+    const f32x2 om = pk_fma(-(t[j] * ez), q[j], splat2(1.0f));
+#else
     const f32x2 om = splat2(1.0f) - (t[j] * ez) * q[j];
+#endif
     w[j] = splat2(1.0f) +
            f32x2{__builtin_copysignf(om.x, zq[j].x), __builtin_copysignf(om.y, zq[j].y)};
   }

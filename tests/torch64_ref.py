@@ -80,13 +80,13 @@ def kernel_probit_prob(t32, base32, form):
     for ck in c[2:]:
         p = _fma(t, p.to(F64), ck)
     z64 = zq.to(F64)
+    # om = 1 - erfc as one fma of the unrounded product (MPV_OM_FMA)
     if form == "p":
         a = (-z64 * z64 + p.to(F64)).to(F32)
-        erfc = (t * torch.exp2(a.to(F64)).to(F32).to(F64)).to(F32)
+        om = _fma(-t, torch.exp2(a.to(F64)).to(F32).to(F64), 1.0)
     else:
         ez = torch.exp2((-z64 * z64).to(F32).to(F64)).to(F32)
-        erfc = ((t * ez.to(F64)).to(F32).to(F64) * p.to(F64)).to(F32)
-    om = (1.0 - erfc.to(F64)).to(F32)
+        om = _fma(-(t * ez.to(F64)).to(F32).to(F64), p.to(F64), 1.0)
     w = (1.0 + torch.copysign(om, zq).to(F64)).to(F32)
     return ((w.to(F64) * _KEH).to(F32).to(F64) + float(_C0)).to(F32)
 
