@@ -51,7 +51,7 @@ struct FwdParams {
 // Tuning constants of the product kernels (each measured; DESIGN.md section 3
 // lists the variants that lost and were removed):
 // fwd_combine: one block per batch row (512 / 256 threads: C4 0.076 -> 0.115 /
-// 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3)
+// 0.188 ms, C3 0.023 -> 0.027 / 0.038 ms; round 3; 512 at C2 / C3 +-0, round 6)
 #ifndef MPV_COMBINE_THREADS
 #define MPV_COMBINE_THREADS 1024
 #endif
@@ -64,29 +64,37 @@ constexpr int kEpiSampleBlocks = 5;    // epilogue: sample blocks between schedu
 // 128: 26.8; round 5's MFMA-layout 48 x 128 tile, two workgroups per CU
 // without packed fp32: 33.4; same box, eager)
 constexpr int kFwd48BM = 256;
+// The 256 x 256 tile (probit_fwd16b, L > 128 and S >= 256; round 6, same-box
+// A/Bs in profiles/r06_fwd16b_ab.json), C4 forward ms against 13.60 for the
+// 256 x 128 tile:
+//   kFwdBA    sample blocks of waves 0-3 (of 16): 8 -> 13.07, 9 and 10 -> 12.79;
+//             11 and 12 spill
+//   kFwdBPart sample blocks per epilogue part: 1 -> 13.44, 2 -> 12.79
+//   kFwdBCQ   column-sum slots per 16-lane row: 4 (lane quads) -> 12.58
+//   kFwdBEpi, kFwdBUnroll: the label loop's scheduling knobs (fwd_tile_epilogue_t)
 #ifndef MPV_FWD_B
 #define MPV_FWD_B 1
 #endif
 #ifndef MPV_FWD_BA
 #define MPV_FWD_BA 10
 #endif
-constexpr bool kFwdB = MPV_FWD_B;  // L > 128: the 256 x 256 tile (probit_fwd16b)
-constexpr int kFwdBA = MPV_FWD_BA;  // its sample blocks on waves 0-3 (of 16)
+#ifndef MPV_FWD_BPART
+#define MPV_FWD_BPART 2
+#endif
+#ifndef MPV_FWD_BCQ
+#define MPV_FWD_BCQ 4
+#endif
 #ifndef MPV_FWD_BEPI
 #define MPV_FWD_BEPI 2
 #endif
 #ifndef MPV_FWD_BUNROLL
 #define MPV_FWD_BUNROLL 0
 #endif
+constexpr bool kFwdB = MPV_FWD_B;
+constexpr int kFwdBA = MPV_FWD_BA;
+constexpr int kFwdBPart = MPV_FWD_BPART;
+constexpr int kFwdBCQ = MPV_FWD_BCQ;
 constexpr int kFwdBEpi = MPV_FWD_BEPI;
-#ifndef MPV_FWD_BPART
-#define MPV_FWD_BPART 2
-#endif
-constexpr int kFwdBPart = MPV_FWD_BPART;  // sample blocks per epilogue part of the 16b tile
-#ifndef MPV_FWD_BCQ
-#define MPV_FWD_BCQ 4
-#endif
-constexpr int kFwdBCQ = MPV_FWD_BCQ;  // column-sum slots per 16-lane row (1: lane 15, 4: quads)
 constexpr bool kFwdBUnroll = MPV_FWD_BUNROLL;
 
 constexpr int kBK = 32;   // fp32 mode: K (= z) chunk staged in LDS
