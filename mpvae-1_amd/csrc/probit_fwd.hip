@@ -1232,15 +1232,18 @@ __global__ __launch_bounds__(512, 1) void probit_fwd16a_kernel(FwdParams p) {
   fwd16t_colpart<WS, BN>(p, cacc, b, sc, n0, NW * 64);
 }
 
-// ------------------ 3xf16, 256 labels x 256 samples (probit_fwd16b, study)
-// probit_fwd16a with twice the samples per tile: the stage image streams
+// ------------- 3xf16, 256 labels x 256 samples (probit_fwd16b, the C4/C5 tile)
+// probit_fwd16a with twice the samples per tile (dispatched for L > 128 and
+// S >= 256; C4 forward 13.6 -> 12.5 ms, round 6): the stage image streams
 // (256 + 256) rows for 256 x 256 x 32 products instead of (256 + 128) for
 // 256 x 128 x 32 (a third fewer operand bytes per product), and each wave's
 // fragment reads cover 64 x TS*16 products.  The accumulators (TL x TSW
 // blocks) leave room for all R fragments of a stage but not all eps ones, so
 // the eps fragments of one 16-sample block are read right before its
 // products (one block ahead).  The row-statistics exchange (red, 24 KB)
-// lives in the stage image the tile's last K stage was read from.
+// lives in the stage image the tile's last K stage was read from; the
+// epilogue runs in parts of kFwdBPart sample blocks.
+//
 // Fwd16Dma for S >= BM (no row clamp): the pieces of one operand image are
 // 32 rows apart, and (r >> 1) & 7 repeats every 16 rows, so every piece of an
 // image has the same per-lane offset from its (wave-uniform) row base -- two
