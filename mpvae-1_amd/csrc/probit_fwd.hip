@@ -1378,7 +1378,7 @@ MPV_DEV void fwd16b_tiles(const FwdParams& p, char* smem, float* cacc, const flo
     // the image of stage gs-1 (read last) is free until the next tile's first
     // barrier; stage gs streams into the other one meanwhile
     float* red = reinterpret_cast<float*>(smem + ((gs + NSTAGE - 1) % NSTAGE) * STAGE);
-    // in kFwdBParts parts of the wave's sample blocks (the row statistics of
+    // in parts of kFwdBPart sample blocks (the row statistics of
     // one part in registers at a time)
     fwd16b_epilogue_parts<0, (TSW / kFwdBPart > 0 ? TSW / kFwdBPart : 1), TL, TSW, BM>(p, acc, scale, b, s0, st * BM, nt, red, cacc,
                                                       cols, soft_any, sbo);
