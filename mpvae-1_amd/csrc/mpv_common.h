@@ -238,12 +238,17 @@ MPV_DEV void probit_prob2xN(const f32x2 (&u)[N], f32x2 (&E)[N]) {
 // of a second exponential of P(t).  fp32-emulated E error over |u| <= 40:
 // max 2.4e-6 (the forward's P form 2.6e-6, NR 2.46e-6).
 constexpr int kErfcxDeg = 6;
+constexpr float kErfcxC1 = -0.359859836f;  // c[1] below
+// qc1: c[1] as a caller-held register pair (a loop keeps it live instead of
+// re-copying the constant into a VGPR every row), or null.
 template <int N>
-MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&ezo)[N]) {
+MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&ezo)[N],
+                             const f32x2* qc1 = nullptr) {
 #pragma clang fp contract(off)
   constexpr float c[kErfcxDeg + 1] = {0.0899837102f, -0.359859836f, 0.38748431f,
                                       0.0453561664f, 0.275197459f,  0.279788422f,
                                       0.282049996f};
+  static_assert(c[1] == kErfcxC1, "qc1 callers hold c[1]");
   f32x2 t[N], q[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -251,7 +256,7 @@ MPV_DEV void probit_dw2xN_zq(const f32x2 (&zq)[N], f32x2 (&w)[N], f32x2 (&ezo)[N
                  fast_rcp(fmaf(0.5f / kSqL2e, fabsf(zq[j].y), 1.0f))};
   }
 #pragma unroll
-  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], splat2(c[0]), splat2(c[1]));
+  for (int j = 0; j < N; ++j) q[j] = pk_fma(t[j], splat2(c[0]), qc1 ? *qc1 : splat2(c[1]));
 #pragma unroll
   for (int k = 2; k <= kErfcxDeg; ++k)
 #pragma unroll

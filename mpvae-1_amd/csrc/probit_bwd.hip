@@ -186,13 +186,15 @@ struct ElemCol {
 // rkp, rkn: the row's ranking coefficients of a positive / negative label,
 // kp (-betaP) and kn betaN (a binary block picks one per column instead of
 // forming wn rkn + wp rkp; elem_rank_coefs).
+// rkq: the four columns' ranking coefficients already picked (the LDS-ring
+// loop reads each from its own address), or null.
 template <bool SOFT = true, bool NANCHK = true, bool SOFT_RCP = false>
 MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2 rkp, f32x2 rkn,
-                       f32x2 (&out)[4]) {
+                       f32x2 (&out)[4], const f32x2* rkq = nullptr, const f32x2* qc1 = nullptr) {
   f32x2 zq[4], w[4], ez[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) zq[q] = pk_fma(splat2(t[q]), splat2(kZq), c.base[q]);
-  probit_dw2xN_zq<4>(zq, w, ez);
+  probit_dw2xN_zq<4>(zq, w, ez, qc1);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     // E in the reference's rounding order (mpvae.py:171-180: cdf = 0.5 (1 +
@@ -221,8 +223,9 @@ MPV_DEV void d_elem2x4(const float (&t)[4], const ElemCol& c, f32x2 alpha, f32x2
       dE = pk_fma(alpha, r, c.gind[q]);
     }
     // ranking term: pos -> -betaP e^{-5E}, neg -> +betaN e^{5E}
-    const f32x2 rk = SOFT ? pk_fma(splat2(c.wn[q]), rkn, splat2(c.wp[q]) * rkp)
-                          : (c.pos[q] ? rkp : rkn);
+    const f32x2 rk = rkq   ? rkq[q]
+                     : SOFT ? pk_fma(splat2(c.wn[q]), rkn, splat2(c.wp[q]) * rkp)
+                            : (c.pos[q] ? rkp : rkn);
     const f32x2 a = w[q] * c.sga[q];
     dE = pk_fma(rk, f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}, dE);
     out[q] = dE * ez[q];  // the coefficients carry kPhiK
@@ -417,6 +420,9 @@ __global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p
 constexpr int kElemRing = 8;       // T rows in flight per wave (1 KB each; 8: 3 waves per SIMD)
 constexpr int kElemRingRows = 256;  // rows per sub-chunk (the coefficient copy)
 constexpr int kElemRingMinRows = 128;  // rows per block at least (plan_bwd; 64: +0.3 % at S 512)
+#ifndef MPV_ELEM_SEL
+#define MPV_ELEM_SEL 1  // per-lane ranking-coefficient addresses, scalar-base stores
+#endif
 // The rows of one sub-chunk [sb, sb + nrows) for one wave; SOFT: the block
 // holds soft labels (block-uniform, so either loop is one basic block).
 // MASK: some lane of the wave has columns past L or past the planes (their G is
@@ -442,14 +448,44 @@ MPV_DEV void elem_ring_rows(const ElemParams& p, const ElemCol& ec, const bool (
   };
   const int pro = min(NR, nrows);
   for (int r = 0; r < pro; ++r) issue(r);
+#if MPV_ELEM_SEL
+  // each column's ranking coefficient read from its own cf address (rkp at
+  // byte 0 of a row, rkn at 16; alpha at 8 and 24, so 8 past either): no
+  // per-row select
+  uint32_t rsel[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rsel[q] = ec.pos[q] ? 0u : 16u;
+  // the lane's plane offset in a row (bytes); the row base is wave-uniform
+  const uint32_t loffb = live ? 2u * (uint32_t)(((c0 >> 5) << 6) + (c0 & 31)) : 0u;
+  f32x2 qc1 = splat2(kErfcxC1);
+  asm volatile("" : "+v"(qc1));
+#endif
   auto row = [&](int r) {
     const f32x4 tv = *reinterpret_cast<const f32x4*>(myring + (r % NR) * 256 + lane * 4);
+    const float t[4] = {tv[0], tv[1], tv[2], tv[3]};
+    f32x2 g2[4];
+#if MPV_ELEM_SEL
+    // (the row offset opaque: a scalar, so each address is one add)
+    const char* crow =
+        reinterpret_cast<const char*>(&cf[0][0]) + __builtin_amdgcn_readfirstlane(r * 32);
+    const f32x2 rkp = *reinterpret_cast<const f32x2*>(crow);
+    const f32x2 rkn = *reinterpret_cast<const f32x2*>(crow + 16);
+    if (SOFT) {
+      const f32x2 alpha = *reinterpret_cast<const f32x2*>(crow + 8);
+      d_elem2x4<SOFT, false, true>(t, ec, alpha, rkp, rkn, g2);
+    } else {
+      f32x2 rkq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rkq[q] = *reinterpret_cast<const f32x2*>(crow + rsel[q]);
+      const f32x2 alpha = *reinterpret_cast<const f32x2*>(crow + rsel[0] + 8);
+      d_elem2x4<SOFT, false, true>(t, ec, alpha, rkp, rkn, g2, rkq, &qc1);
+    }
+#else
     const f32x4 ca = *reinterpret_cast<const f32x4*>(&cf[r][0]);
     const f32x2 rkn = *reinterpret_cast<const f32x2*>(&cf[r][4]);
     const f32x2 alpha = f32x2{ca[0], ca[1]}, rkp = f32x2{ca[2], ca[3]};
-    const float t[4] = {tv[0], tv[1], tv[2], tv[3]};
-    f32x2 g2[4];
     d_elem2x4<SOFT, false, true>(t, ec, alpha, rkp, rkn, g2);
+#endif
     // a degenerate row poisons every label (the row's rkp is wave-uniform)
     if (NANCHK && __builtin_amdgcn_readfirstlane((rkp.x != rkp.x || rkp.y != rkp.y) ? 1 : 0)) {
 #pragma unroll
@@ -468,11 +504,30 @@ MPV_DEV void elem_ring_rows(const ElemParams& p, const ElemCol& ec, const bool (
     uint32_t hv[2], lv[2];
     split2_f16(G[0], G[1], gs, hv[0], lv[0]);
     split2_f16(G[2], G[3], gs, hv[1], lv[1]);
+#if MPV_ELEM_SEL
+    // the row base made opaque so it stays a scalar base (saddr stores with a
+    // 32-bit lane offset, no 64-bit address add per row)
+    const uint64_t ga = reinterpret_cast<uint64_t>(p.g + (rowb + r) * p.gld);
+    // (readfirstlane returns int: each half zero-extended through uint32_t)
+    const uint64_t grow =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ga >> 32)) << 32) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ga);
+    if (!MASK || live) {  // nontemporal plane stores (the element pass -2 %, round 2)
+      // (asm: hipcc forms a 64-bit lane address per row otherwise; the ring's
+      // vmcnt arithmetic counts these two stores as before)
+      asm volatile("global_store_dwordx2 %0, %1, %2 nt\n\t"
+                   "global_store_dwordx2 %0, %3, %2 offset:%4 nt"
+                   :
+                   : "v"(loffb), "v"(u32x2{hv[0], hv[1]}), "s"(grow), "v"(u32x2{lv[0], lv[1]}),
+                     "i"(2 * kLoOff));
+    }
+#else
     const int64_t o = chunked_index(rowb + r, p.gld, live ? c0 : 0);
     if (!MASK || live) {  // nontemporal plane stores (the element pass -2 %, round 2)
       __builtin_nontemporal_store(u32x2{hv[0], hv[1]}, reinterpret_cast<u32x2*>(p.g + o));
       __builtin_nontemporal_store(u32x2{lv[0], lv[1]}, reinterpret_cast<u32x2*>(p.g + o + kLoOff));
     }
+#endif
     if (r + NR < nrows) issue(r + NR);  // into the slot row r was just read from
   };
   // Before row r is read, the ops issued after its DMA are the DMAs of rows
@@ -541,8 +596,13 @@ __global__ __launch_bounds__(256, 3) void bwd_elem_ring_kernel(ElemParams p) {
       f32x2 rkp, rkn;
       elem_rank_coefs(ec, bP, bN, rkp, rkn);
       nan_row |= bP.x != bP.x || bP.y != bP.y;
+#if MPV_ELEM_SEL
+      *reinterpret_cast<f32x4*>(&cf[r][0]) = f32x4{rkp.x, rkp.y, alpha.x, alpha.y};
+      *reinterpret_cast<f32x4*>(&cf[r][4]) = f32x4{rkn.x, rkn.y, alpha.x, alpha.y};
+#else
       *reinterpret_cast<f32x4*>(&cf[r][0]) = f32x4{alpha.x, alpha.y, rkp.x, rkp.y};
       *reinterpret_cast<f32x2*>(&cf[r][4]) = rkn;
+#endif
     }
     const bool nan_any = __syncthreads_or(nan_row) != 0;
     if (!wave_live) continue;
