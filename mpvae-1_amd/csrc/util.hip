@@ -484,7 +484,13 @@ constexpr float kNoiseScale = 4096.0f;
 // call when z % 4 == 0, else words of two calls), stored as two 16-B vectors.
 // Planes narrower than 8 x blockDim columns give each row cols/8 threads and
 // the block several rows at once.
-constexpr int kNoiseRows = 16;  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4)
+#ifndef MPV_NOISE_ROWS
+#define MPV_NOISE_ROWS 16
+#endif
+#ifndef MPV_NOISE_NT
+#define MPV_NOISE_NT 0  // nontemporal plane stores: 1.69 -> 2.61 ms at C4 (r06_noise_ab.json)
+#endif
+constexpr int kNoiseRows = MPV_NOISE_ROWS;  // plane rows per block (1: 2.08 ms, 4: 1.99, 16: 1.93 at C4; 8, 32: as 16)
 constexpr int kNoiseCols = 8;   // plane columns per thread (4: 1.78 ms, 8: 1.69 ms at C4)
 #ifndef MPV_NOISE_PASSES
 #define MPV_NOISE_PASSES 2
@@ -582,8 +588,13 @@ MPV_DEV void noise16_row(const mpv_split16& out, int S, int B, int z, int64_t s_
                    (short)h[4], (short)h[5], (short)h[6], (short)h[7]};
     const s16x8 lv{(short)l[0], (short)l[1], (short)l[2], (short)l[3],
                    (short)l[4], (short)l[5], (short)l[6], (short)l[7]};
+#if MPV_NOISE_NT
+    __builtin_nontemporal_store(hv, reinterpret_cast<s16x8*>(out.data + o));
+    __builtin_nontemporal_store(lv, reinterpret_cast<s16x8*>(out.data + o + kLoOff));
+#else
     *reinterpret_cast<s16x8*>(out.data + o) = hv;
     *reinterpret_cast<s16x8*>(out.data + o + kLoOff) = lv;
+#endif
   }
 }
 
