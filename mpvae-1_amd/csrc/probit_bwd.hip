@@ -309,7 +309,10 @@ MPV_DEV void elem_col_setup(const ElemParams& p, int b, int c0, bool active, boo
 // the six per-row coefficients are wave-uniform (scalar loads, no VGPRs).
 // Otherwise (L < 1024: C2, C3) they are per-lane, 12 more VGPRs than fit in
 // 128: those instantiations run at 3 waves per SIMD instead of spilling.
-constexpr int kElemLookahead = 1;
+#ifndef MPV_ELEM_LA
+#define MPV_ELEM_LA 1
+#endif
+constexpr int kElemLookahead = MPV_ELEM_LA;  // 2, 3: C3 element pass 0.111 -> 0.120 ms (r06_la_ab.json)
 #ifndef MPV_ELEM_MIN_ROWS
 #define MPV_ELEM_MIN_ROWS 16
 #endif
