@@ -317,8 +317,11 @@ constexpr int kElemLookahead = MPV_ELEM_LA;  // 2, 3: C3 element pass 0.111 -> 0
 #define MPV_ELEM_MIN_ROWS 16
 #endif
 constexpr int kElemMinRows = MPV_ELEM_MIN_ROWS;  // minimum T rows per thread (C2 -6 %)
+#ifndef MPV_ELEM_OCC4
+#define MPV_ELEM_OCC4 0  // 4 waves per SIMD for per-lane rows too: slower (r06_elem_occ4_ab.json)
+#endif
 template <bool VEC, bool PLANES, bool ONE>
-__global__ __launch_bounds__(256, ONE ? 4 : 3) void bwd_elem_kernel(ElemParams p) {
+__global__ __launch_bounds__(256, (ONE || MPV_ELEM_OCC4) ? 4 : 3) void bwd_elem_kernel(ElemParams p) {
   constexpr int LA = kElemLookahead;
   __shared__ float cred[256 * 8];
   const int b = blockIdx.x, sc = blockIdx.y;
